@@ -1,0 +1,39 @@
+# Builds libcocoa_hip.so (gfx950) and the CPU oracle.  Used by
+# __graft_entry__.build(); `make -j8` works standalone too.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := cocoa_amd/csrc
+OUT := cocoa_amd/libcocoa_hip.so
+BUILD := build/obj
+COMMON := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude -I$(CSRC)
+HDRS := $(wildcard $(CSRC)/*.h) include/cocoa_capi.h
+
+all: $(OUT) oracle/liboracle.so cocoa_amd/cocoa_driver
+
+$(BUILD)/%.strict.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(COMMON) -ffp-contract=off -c $< -o $@
+
+$(BUILD)/%.fast.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(COMMON) -ffp-contract=fast -munsafe-fp-atomics -c $< -o $@
+
+$(BUILD)/dataset.o: $(CSRC)/dataset.cpp $(HDRS) | $(BUILD)
+	$(HIPCC) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -I$(CSRC) -x c++ -c $< -o $@
+
+OBJS := $(BUILD)/kernels_strict.strict.o $(BUILD)/kernels_fast.fast.o $(BUILD)/engine.strict.o $(BUILD)/dataset.o
+
+$(OUT): $(OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lpthread
+
+cocoa_amd/cocoa_driver: $(CSRC)/driver_main.cpp $(OUT) include/cocoa_capi.h
+	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude -x c++ $< -o $@ -Lcocoa_amd -lcocoa_hip -Wl,-rpath,'$$ORIGIN'
+
+oracle/liboracle.so: oracle/cocoa_oracle.c
+	$(MAKE) -s -C oracle
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+clean:
+	rm -rf build $(OUT) cocoa_amd/cocoa_driver oracle/liboracle.so
+
+.PHONY: all clean

@@ -1,0 +1,798 @@
+// libcocoa_hip.so engine: device context, data upload, per-round orchestration
+// of the HIP kernels, and the C ABI declared in include/cocoa_capi.h.
+//
+// Round structure on one rank (CoCoA.scala:39-63):
+//   sampler      java.util.Random(seed+t).nextInt(n_k) x H per partition
+//   solver       K_loc local solvers (one 2-wave workgroup per partition)
+//   fold         ordered sum of the private deltaW slices (zeroing them)
+//   [caller all-reduces the sum across ranks]           (multi-GPU only)
+//   apply        w += sum * scaling
+// Host arithmetic in this file (objective assembly, row norms) is compiled
+// with -ffp-contract=off like the strict kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cocoa_capi.h"
+#include "common.h"
+#include "jrandom.h"
+#include "kernels.h"
+
+using namespace cocoa;
+
+static std::mutex g_err_mu;
+static std::string g_err;
+void cocoa_set_global_error(const std::string& msg) {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    g_err = msg;
+}
+
+#define HIPCHK(x)                                                                                        \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess)                                                                            \
+            throw Error(COCOA_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_) + " at " __FILE__ ":" + \
+                                         std::to_string(__LINE__));                                      \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void alloc(size_t b) {
+        free();
+        if (b == 0) b = 16;
+        HIPCHK(hipMalloc(&p, b));
+        bytes = b;
+    }
+    void alloc_zero(size_t b, hipStream_t s) {
+        alloc(b);
+        HIPCHK(hipMemsetAsync(p, 0, bytes, s));
+    }
+    void free() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return (T*)p;
+    }
+    ~DevBuf() { free(); }
+};
+
+struct Csr {
+    int64_t n = 0, nnz = 0;
+    DevBuf row_ptr, col, val, y;
+};
+
+constexpr size_t kLdsMax = 160 * 1024;
+constexpr int kStreamCap = 2048;
+
+size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+}  // namespace
+
+struct cocoa_ctx {
+    int device = 0;
+    bool strict = false;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+
+    // training data (this rank)
+    int32_t K_loc = 0, K_glob = 0, part_begin = 0, d = 0;
+    Csr tr;
+    DevBuf sqn, rowflags, part_ptr;
+    std::vector<int64_t> h_part_ptr;
+    bool any_dup = false;
+    int32_t max_nl = 0, min_nl = 0;
+    // test data (this rank)
+    Csr te;
+    bool has_test = false;
+
+    // run state
+    bool inited = false;
+    int method = 0;
+    cocoa_params P{};
+    cocoa_debug D{};
+    double scaling = 1.0, mult = 1.0;
+    DevBuf w, alpha, alpha_work, dw, wloc, samples, dw_sum_int, eval_part, eval_out, row_scratch, jump;
+    double* dw_sum = nullptr;
+    double* h_eval = nullptr;  // pinned [4]
+    int64_t samples_cap = 0;
+
+    // solver plan
+    bool vec_lds = false, alpha_lds = false;
+    size_t lds_bytes = 0;
+    SolverArgs sa{};
+
+    // stats
+    bool stats = false;
+    struct Pending {
+        int kid;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    double tot_ms[COCOA_K_COUNT] = {0};
+    int64_t cnt[COCOA_K_COUNT] = {0};
+
+    hipEvent_t get_ev() {
+        if (!ev_pool.empty()) {
+            hipEvent_t e = ev_pool.back();
+            ev_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        return e;
+    }
+    template <class F>
+    void timed(int kid, F&& f) {
+        if (!stats) {
+            f();
+            HIPCHK(hipGetLastError());
+            return;
+        }
+        hipEvent_t a = get_ev(), b = get_ev();
+        HIPCHK(hipEventRecord(a, stream));
+        f();
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(b, stream));
+        pending.push_back({kid, a, b});
+        if (pending.size() > 4096) drain();
+    }
+    void drain() {
+        for (auto& p : pending) {
+            HIPCHK(hipEventSynchronize(p.b));
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+            tot_ms[p.kid] += ms;
+            cnt[p.kid] += 1;
+            ev_pool.push_back(p.a);
+            ev_pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+    ~cocoa_ctx() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto& p : pending) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (auto e : ev_pool) (void)hipEventDestroy(e);
+        if (h_eval) (void)hipHostFree(h_eval);
+        if (own_stream && stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+#define CAPI_BEGIN(ctx)                                             \
+    if (!(ctx)) {                                                   \
+        cocoa_set_global_error("null context");                     \
+        return COCOA_E_ARG;                                         \
+    }                                                               \
+    try {                                                           \
+        HIPCHK(hipSetDevice((ctx)->device));
+#define CAPI_END(ctx)                                               \
+    return COCOA_OK;                                                \
+    }                                                               \
+    catch (const Error& e) {                                        \
+        (ctx)->err = e.what();                                      \
+        cocoa_set_global_error(e.what());                           \
+        return e.code;                                              \
+    }                                                               \
+    catch (const std::exception& e) {                               \
+        (ctx)->err = e.what();                                      \
+        cocoa_set_global_error(e.what());                           \
+        return COCOA_E_ARG;                                         \
+    }
+
+static void require(bool cond, int code, const std::string& msg) {
+    if (!cond) throw Error(code, msg);
+}
+
+// ---------------------------------------------------------------- context --
+extern "C" int cocoa_version(void) { return COCOA_CAPI_VERSION; }
+
+extern "C" const char* cocoa_last_error(const cocoa_ctx* ctx) {
+    if (ctx) return ctx->err.c_str();
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    static thread_local std::string copy;
+    copy = g_err;
+    return copy.c_str();
+}
+
+extern "C" int cocoa_create(int device, int strict, void* stream, cocoa_ctx** out) {
+    if (!out) return COCOA_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        cocoa_set_global_error("no HIP device available (libcocoa_hip needs an MI355X / gfx950 GPU)");
+        return COCOA_E_NODEV;
+    }
+    if (device < 0 || device >= ndev) {
+        cocoa_set_global_error("device ordinal out of range");
+        return COCOA_E_ARG;
+    }
+    cocoa_ctx* c = new cocoa_ctx();
+    c->device = device;
+    c->strict = strict != 0;
+    try {
+        HIPCHK(hipSetDevice(device));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            throw Error(COCOA_E_NODEV, std::string("libcocoa_hip is built for gfx950; device is ") + prop.gcnArchName);
+        if (stream) {
+            c->stream = (hipStream_t)stream;
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            c->own_stream = true;
+        }
+        HIPCHK(hipHostMalloc((void**)&c->h_eval, 8 * sizeof(double), hipHostMallocDefault));
+        // jump table (A_j, C_j), j = 1..256, for the sampler
+        std::vector<uint64_t> jt(512);
+        for (int j = 1; j <= 256; ++j) jr_jump((uint64_t)j, &jt[2 * (j - 1)], &jt[2 * (j - 1) + 1]);
+        c->jump.alloc(jt.size() * sizeof(uint64_t));
+        HIPCHK(hipMemcpy(c->jump.p, jt.data(), jt.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    } catch (const Error& e) {
+        cocoa_set_global_error(e.what());
+        delete c;
+        return e.code;
+    }
+    *out = c;
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_destroy(cocoa_ctx* ctx) {
+    if (!ctx) return COCOA_OK;
+    (void)hipSetDevice(ctx->device);
+    delete ctx;
+    return COCOA_OK;
+}
+
+static void upload(DevBuf& b, const void* src, size_t bytes, hipStream_t s) {
+    b.alloc(bytes);
+    if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s));
+}
+
+static void check_csr(const int64_t* row_ptr, const int32_t* col, int64_t n, int32_t d) {
+    require(row_ptr[0] == 0, COCOA_E_ARG, "row_ptr[0] must be 0");
+    for (int64_t r = 0; r < n; ++r) require(row_ptr[r + 1] >= row_ptr[r], COCOA_E_ARG, "row_ptr not monotone");
+    const int64_t nnz = row_ptr[n];
+    for (int64_t q = 0; q < nnz; ++q)
+        if (col[q] < 0 || col[q] >= d)
+            throw Error(COCOA_E_RANGE, "ArrayIndexOutOfBoundsException: feature index " + std::to_string(col[q]) +
+                                           " outside [0," + std::to_string(d) + ")");
+}
+
+// ------------------------------------------------------------------- data --
+extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const int64_t* row_ptr,
+                               const int32_t* col, const double* val, const double* y, int64_t n_rows,
+                               int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
+    CAPI_BEGIN(ctx)
+    require(num_parts >= 1 && part_ptr && row_ptr && y && n_rows >= 0 && num_features >= 1, COCOA_E_ARG,
+            "cocoa_set_train: bad argument");
+    require(part_begin >= 0 && num_parts_global >= part_begin + num_parts, COCOA_E_ARG,
+            "cocoa_set_train: bad partition range");
+    require(part_ptr[0] == 0 && part_ptr[num_parts] == n_rows, COCOA_E_ARG, "part_ptr must span [0, n_rows]");
+    for (int k = 0; k < num_parts; ++k) require(part_ptr[k + 1] >= part_ptr[k], COCOA_E_ARG, "part_ptr not monotone");
+    check_csr(row_ptr, col, n_rows, num_features);
+    const int64_t nnz = row_ptr[n_rows];
+    ctx->K_loc = num_parts;
+    ctx->K_glob = num_parts_global;
+    ctx->part_begin = part_begin;
+    ctx->d = num_features;
+    ctx->tr.n = n_rows;
+    ctx->tr.nnz = nnz;
+    ctx->h_part_ptr.assign(part_ptr, part_ptr + num_parts + 1);
+    ctx->max_nl = 0;
+    ctx->min_nl = INT32_MAX;
+    for (int k = 0; k < num_parts; ++k) {
+        const int64_t nl = part_ptr[k + 1] - part_ptr[k];
+        require(nl <= INT32_MAX, COCOA_E_ARG, "partition too large");
+        ctx->max_nl = std::max<int32_t>(ctx->max_nl, (int32_t)nl);
+        ctx->min_nl = std::min<int32_t>(ctx->min_nl, (int32_t)nl);
+    }
+    // Math.pow(x.norm(2), 2) per row (CoCoA.scala:173), in stored order; and
+    // duplicate-column flags (rows whose scatter must stay sequential)
+    std::vector<double> sq((size_t)std::max<int64_t>(n_rows, 1));
+    std::vector<uint8_t> fl((size_t)std::max<int64_t>(n_rows, 1), 0);
+    ctx->any_dup = false;
+    std::vector<int64_t> seen_at((size_t)num_features, -1);
+    for (int64_t r = 0; r < n_rows; ++r) {
+        double s = 0.0;
+        bool sorted = true;
+        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) {
+            s += val[q] * val[q];
+            if (q > row_ptr[r] && col[q] <= col[q - 1]) sorted = false;
+        }
+        const double nr = std::sqrt(s);
+        sq[(size_t)r] = nr * nr;
+        if (!sorted) {
+            for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) {
+                if (seen_at[(size_t)col[q]] == r) fl[(size_t)r] = 1;
+                seen_at[(size_t)col[q]] = r;
+            }
+            if (fl[(size_t)r]) ctx->any_dup = true;
+        }
+    }
+    hipStream_t s = ctx->stream;
+    upload(ctx->tr.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
+    upload(ctx->tr.col, col, sizeof(int32_t) * (size_t)nnz, s);
+    upload(ctx->tr.val, val, sizeof(double) * (size_t)nnz, s);
+    upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
+    upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
+    upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
+    upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->inited = false;
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t* col, const double* val,
+                              const double* y, int64_t n_rows) {
+    CAPI_BEGIN(ctx)
+    require(ctx->d > 0, COCOA_E_STATE, "cocoa_set_test: call cocoa_set_train first");
+    require(row_ptr && y && n_rows >= 0, COCOA_E_ARG, "cocoa_set_test: bad argument");
+    check_csr(row_ptr, col, n_rows, ctx->d);
+    const int64_t nnz = row_ptr[n_rows];
+    hipStream_t s = ctx->stream;
+    ctx->te.n = n_rows;
+    ctx->te.nnz = nnz;
+    upload(ctx->te.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
+    upload(ctx->te.col, col, sizeof(int32_t) * (size_t)nnz, s);
+    upload(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
+    upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->has_test = true;
+    if (ctx->inited) {
+        const size_t rows = (size_t)(ctx->tr.n + ctx->te.n);
+        ctx->row_scratch.alloc(sizeof(double) * std::max<size_t>(rows, 1));
+    }
+    CAPI_END(ctx)
+}
+
+// ----------------------------------------------------------------- solver --
+static bool is_sdca(int m) { return m == COCOA_METHOD_COCOA_PLUS || m == COCOA_METHOD_COCOA || m == COCOA_METHOD_MBCD; }
+static int solver_mode(int m) {
+    return m == COCOA_METHOD_COCOA_PLUS ? MODE_PLUS : m == COCOA_METHOD_COCOA ? MODE_COCOA : MODE_MBCD;
+}
+static int32_t wrap32(int64_t x) { return (int32_t)(uint32_t)(uint64_t)x; }
+
+static void plan_solver(cocoa_ctx* c) {
+    SolverArgs& a = c->sa;
+    size_t off = 0;
+    const size_t vec_bytes = align16(sizeof(double) * (size_t)c->d);
+    const size_t cap = kStreamCap;
+    const size_t fixed = 2 * align16(cap * 4) + 2 * align16(cap * 8) + 2 * align16(sizeof(BatchMeta)) +
+                         align16(cap * 8) + align16(sizeof(double) * kRegChunks * 64);
+    size_t avail = kLdsMax - fixed;
+    c->vec_lds = is_sdca(c->method) && vec_bytes <= avail;
+    if (c->vec_lds) avail -= vec_bytes;
+    const size_t al_bytes = align16(sizeof(double) * (size_t)std::max(c->max_nl, 1));
+    c->alpha_lds = is_sdca(c->method) && al_bytes <= avail;
+    if (c->vec_lds) {
+        a.lds_vec = (int32_t)off;
+        off += vec_bytes;
+    }
+    for (int b = 0; b < 2; ++b) {
+        a.lds_stream_val[b] = (int32_t)off;
+        off += align16(cap * 8);
+        a.lds_stream_col[b] = (int32_t)off;
+        off += align16(cap * 4);
+        a.lds_meta[b] = (int32_t)off;
+        off += align16(sizeof(BatchMeta));
+    }
+    a.lds_prod = (int32_t)off;
+    off += align16(cap * 8);
+    a.lds_scratch = (int32_t)off;
+    off += align16(sizeof(double) * kRegChunks * 64);
+    if (c->alpha_lds) {
+        a.lds_alpha = (int32_t)off;
+        off += al_bytes;
+    }
+    c->lds_bytes = off;
+    a.stream_cap = (int32_t)cap;
+}
+
+extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
+                          const double* w_init) {
+    CAPI_BEGIN(ctx)
+    require(params && method >= 0 && method <= 4, COCOA_E_ARG, "cocoa_init: bad argument");
+    require(ctx->d > 0 && ctx->K_loc > 0, COCOA_E_STATE, "cocoa_init: no training data");
+    require(params->local_iters >= 0 && params->n >= 1, COCOA_E_ARG, "cocoa_init: bad params");
+    if (params->local_iters >= 1)
+        require(ctx->min_nl >= 1, COCOA_E_ARG,
+                "IllegalArgumentException: empty partition (java.util.Random.nextInt(0), CoCoA.scala:151)");
+    ctx->P = *params;
+    ctx->D = debug ? *debug : cocoa_debug{10, 0, 100, 0};
+    ctx->method = method;
+    const int64_t d = ctx->d, n = ctx->tr.n, K = ctx->K_loc;
+    const int32_t H = params->local_iters;
+    const double Kg = (double)ctx->K_glob;
+    const double kh = (double)wrap32((int64_t)ctx->K_glob * H);  // Scala Int product
+    switch (method) {
+        case COCOA_METHOD_COCOA_PLUS: ctx->scaling = params->gamma; break;       // CoCoA.scala:37
+        case COCOA_METHOD_COCOA: ctx->scaling = params->beta / Kg; break;        // CoCoA.scala:37
+        case COCOA_METHOD_MBCD: ctx->scaling = params->beta / kh; break;         // MinibatchCD.scala:147
+        case COCOA_METHOD_LOCALSGD: ctx->scaling = params->beta / Kg; break;     // SGD.scala:285
+        case COCOA_METHOD_MBSGD: ctx->scaling = params->beta / kh; break;        // SGD.scala:287
+    }
+    hipStream_t s = ctx->stream;
+    ctx->w.alloc(sizeof(double) * (size_t)d);
+    if (w_init)
+        HIPCHK(hipMemcpyAsync(ctx->w.p, w_init, sizeof(double) * (size_t)d, hipMemcpyHostToDevice, s));
+    else
+        HIPCHK(hipMemsetAsync(ctx->w.p, 0, sizeof(double) * (size_t)d, s));
+    ctx->alpha.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
+    ctx->alpha_work.alloc(sizeof(double) * (size_t)std::max<int64_t>(n, 1));
+    ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * d), s);
+    const bool need_wloc = method == COCOA_METHOD_COCOA || method == COCOA_METHOD_LOCALSGD;
+    ctx->method = method;
+    plan_solver(ctx);
+    if (need_wloc && !(method == COCOA_METHOD_COCOA && ctx->vec_lds))
+        ctx->wloc.alloc(sizeof(double) * (size_t)(K * d));
+    else
+        ctx->wloc.free();
+    ctx->samples_cap = std::max<int64_t>((int64_t)K * H, 1);
+    ctx->samples.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
+    ctx->dw_sum_int.alloc(sizeof(double) * (size_t)d);
+    if (!ctx->dw_sum) ctx->dw_sum = ctx->dw_sum_int.as<double>();
+    ctx->eval_part.alloc(sizeof(double) * (size_t)std::max<int64_t>(4 * 2048, 2 * K + 8));
+    ctx->eval_out.alloc(sizeof(double) * 8);
+    ctx->row_scratch.alloc(sizeof(double) * (size_t)std::max<int64_t>(n + ctx->te.n, 1));
+
+    SolverArgs& a = ctx->sa;
+    a.row_ptr = ctx->tr.row_ptr.as<int64_t>();
+    a.col = ctx->tr.col.as<int32_t>();
+    a.val = ctx->tr.val.as<double>();
+    a.y = ctx->tr.y.as<double>();
+    a.sqn = ctx->sqn.as<double>();
+    a.rowflags = ctx->rowflags.as<uint8_t>();
+    a.part_ptr = ctx->part_ptr.as<int64_t>();
+    a.samples = ctx->samples.as<int32_t>();
+    a.alpha = ctx->alpha.as<double>();
+    a.alpha_work = ctx->alpha_work.as<double>();
+    a.w = ctx->w.as<double>();
+    a.dw = ctx->dw.as<double>();
+    a.wloc = ctx->wloc.p ? ctx->wloc.as<double>() : nullptr;
+    a.d = d;
+    a.H = H;
+    a.any_dup = ctx->any_dup ? 1 : 0;
+    a.raw_alpha = 0;
+    a.lam_n = params->lambda * (double)params->n;
+    a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
+    a.scaling = ctx->scaling;
+    HIPCHK(hipStreamSynchronize(s));
+    ctx->inited = true;
+    CAPI_END(ctx)
+}
+
+static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
+    require(c->inited, COCOA_E_STATE, "cocoa_round: call cocoa_init first");
+    const int32_t H = c->P.local_iters;
+    const int32_t seed = wrap32((int64_t)c->D.seed + t);                    // debug.seed + t
+    hipStream_t s = c->stream;
+    const int64_t d = c->d;
+    const int K = c->K_loc;
+    c->mult = c->scaling;
+    if (H >= 1) {
+        c->timed(COCOA_K_SAMPLE, [&] {
+            launch_sampler(c->part_ptr.as<int64_t>(), K, seed, H, c->samples.as<int32_t>(), c->jump.as<uint64_t>(), s);
+        });
+        if (is_sdca(c->method)) {
+            c->timed(COCOA_K_SOLVER, [&] {
+                if (c->strict)
+                    launch_solver_strict(solver_mode(c->method), c->vec_lds, c->alpha_lds, c->sa, K, c->lds_bytes, s);
+                else
+                    launch_solver_fast(solver_mode(c->method), c->vec_lds, c->alpha_lds, c->sa, K, c->lds_bytes, s);
+            });
+        } else {
+            const double step = 1 / (c->P.lambda * (double)t);                 // SGD.scala:293
+            const bool local = c->method == COCOA_METHOD_LOCALSGD;
+            if (!local) {
+                const double scale = 1.0 - (step * c->P.lambda);             // SGD.scala:297-298
+                c->timed(COCOA_K_APPLY, [&] { launch_scale(c->w.as<double>(), d, scale, s); });
+                c->mult = step * c->scaling;                                 // SGD.scala:307
+            }
+            const double t0 = (double)wrap32((int64_t)(t - 1) * H * c->K_glob); // SGD.scala:302 (Int)
+            c->timed(COCOA_K_SOLVER, [&] { launch_sgd(local, c->sa, c->P.lambda, t0, K, s); });
+        }
+    } else if (c->method == COCOA_METHOD_MBSGD) {
+        const double step = 1 / (c->P.lambda * (double)t);
+        c->timed(COCOA_K_APPLY, [&] { launch_scale(c->w.as<double>(), d, 1.0 - (step * c->P.lambda), s); });
+        c->mult = step * c->scaling;
+    }
+    c->timed(COCOA_K_FOLD, [&] {
+        launch_fold(c->dw.as<double>(), K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, s);
+    });
+}
+
+extern "C" int cocoa_round_local(cocoa_ctx* ctx, int32_t t) {
+    CAPI_BEGIN(ctx)
+    run_local(ctx, t, false);
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_dw_sum_device_ptr(cocoa_ctx* ctx, void** out) {
+    CAPI_BEGIN(ctx)
+    require(out != nullptr, COCOA_E_ARG, "null out");
+    require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    *out = (void*)ctx->dw_sum;
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_set_dw_sum_buffer(cocoa_ctx* ctx, void* device_ptr) {
+    CAPI_BEGIN(ctx)
+    ctx->dw_sum = device_ptr ? (double*)device_ptr : ctx->dw_sum_int.as<double>();
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_round_apply(cocoa_ctx* ctx) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    ctx->timed(COCOA_K_APPLY, [&] { launch_apply(ctx->w.as<double>(), ctx->dw_sum, ctx->d, ctx->mult, ctx->stream); });
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_round(cocoa_ctx* ctx, int32_t t) {
+    CAPI_BEGIN(ctx)
+    run_local(ctx, t, true);
+    CAPI_END(ctx)
+}
+
+// ------------------------------------------------------------------- eval --
+static void finish(const cocoa_ctx* c, double hinge, double alpha_sum, double w2, int64_t err, int64_t n_test,
+                   cocoa_eval_result* out) {
+    const double lam = c->P.lambda;
+    const double n = (double)c->P.n;
+    const double nw = std::sqrt(w2);                                          // w.norm(2)
+    const double nw2 = nw * nw;                                               // Math.pow(., 2)
+    out->hinge_sum = hinge;
+    out->alpha_sum = alpha_sum;
+    out->w_sqnorm = w2;                                                       // raw sum of squares
+    out->primal = hinge / n + (0.5 * lam * nw2);                              // OptUtils.scala:73-75
+    out->dual = (-lam / 2 * nw2) + (alpha_sum / n);                           // OptUtils.scala:80-84
+    out->gap = out->primal - out->dual;                                       // OptUtils.scala:89-91
+    out->test_err_count = err;
+    out->test_rows = n_test;
+    out->test_error = n_test > 0 ? (double)err / (double)n_test : NAN;        // OptUtils.scala:95-98
+}
+
+extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
+    CAPI_BEGIN(ctx)
+    require(out != nullptr, COCOA_E_ARG, "null out");
+    require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    EvalArgs e{};
+    e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
+    e.col = ctx->tr.col.as<int32_t>();
+    e.val = ctx->tr.val.as<double>();
+    e.y = ctx->tr.y.as<double>();
+    e.alpha = ctx->alpha.as<double>();
+    e.n = ctx->tr.n;
+    e.t_row_ptr = ctx->has_test ? ctx->te.row_ptr.as<int64_t>() : nullptr;
+    e.t_col = ctx->has_test ? ctx->te.col.as<int32_t>() : nullptr;
+    e.t_val = ctx->has_test ? ctx->te.val.as<double>() : nullptr;
+    e.t_y = ctx->has_test ? ctx->te.y.as<double>() : nullptr;
+    e.n_test = ctx->has_test ? ctx->te.n : 0;
+    e.w = ctx->w.as<double>();
+    e.d = ctx->d;
+    e.part_ptr = ctx->part_ptr.as<int64_t>();
+    e.K = ctx->K_loc;
+    e.partials = ctx->eval_part.as<double>();
+    e.out = ctx->eval_out.as<double>();
+    e.row_scratch = ctx->row_scratch.as<double>();
+    ctx->timed(COCOA_K_EVAL, [&] {
+        if (ctx->strict)
+            launch_eval_strict(e, ctx->stream);
+        else
+            launch_eval_fast(e, eval_fast_blocks(e.n, e.n_test), ctx->stream);
+    });
+    HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    finish(ctx, ctx->h_eval[0], ctx->h_eval[1], ctx->h_eval[2], (int64_t)ctx->h_eval[3], e.n_test, out);
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_eval_finish(const cocoa_ctx* ctx, double hinge_sum, double alpha_sum, double w_sqnorm,
+                                 int64_t test_err_count, int64_t test_rows, cocoa_eval_result* out) {
+    if (!ctx || !out) return COCOA_E_ARG;
+    // w_sqnorm: the raw sum of squares of w (identical on every rank)
+    finish(ctx, hinge_sum, alpha_sum, w_sqnorm, test_err_count, test_rows, out);
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_run(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
+                         const double* w_init, cocoa_round_cb cb, void* user) {
+    int rc = cocoa_init(ctx, params, debug, method, w_init);
+    if (rc) return rc;
+    for (int32_t t = 1; t <= params->num_rounds; ++t) {
+        rc = cocoa_round(ctx, t);
+        if (rc) return rc;
+        if (ctx->D.debug_iter > 0 && t % ctx->D.debug_iter == 0) {              // CoCoA.scala:51
+            cocoa_eval_result ev{};
+            rc = cocoa_eval(ctx, &ev);
+            if (rc) return rc;
+            if (cb) cb(user, t, &ev);
+        }
+    }
+    return cocoa_sync(ctx);
+}
+
+extern "C" int cocoa_sync(cocoa_ctx* ctx) {
+    CAPI_BEGIN(ctx)
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_get_w(cocoa_ctx* ctx, double* w_out) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited && w_out, COCOA_E_STATE, "cocoa_get_w: not initialised");
+    HIPCHK(hipMemcpyAsync(w_out, ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_get_alpha(cocoa_ctx* ctx, double* alpha_out) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited && alpha_out, COCOA_E_STATE, "cocoa_get_alpha: not initialised");
+    if (ctx->tr.n)
+        HIPCHK(hipMemcpyAsync(alpha_out, ctx->alpha.p, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_set_w(cocoa_ctx* ctx, const double* w_in) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited && w_in, COCOA_E_STATE, "cocoa_set_w: not initialised");
+    HIPCHK(hipMemcpyAsync(ctx->w.p, w_in, sizeof(double) * (size_t)ctx->d, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_set_alpha(cocoa_ctx* ctx, const double* alpha_in) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited && alpha_in, COCOA_E_STATE, "cocoa_set_alpha: not initialised");
+    if (ctx->tr.n)
+        HIPCHK(hipMemcpyAsync(ctx->alpha.p, alpha_in, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyHostToDevice,
+                              ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    CAPI_END(ctx)
+}
+
+// ------------------------------------------------- unit: CoCoA.localSDCA --
+extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t local_iters, double lambda, int32_t n,
+                                double* alpha, int32_t seed, int plus, double sigma, double* delta_w,
+                                double* delta_alpha) {
+    CAPI_BEGIN(ctx)
+    require(ctx->d > 0, COCOA_E_STATE, "cocoa_local_sdca: no training data");
+    require(part >= 0 && part < ctx->K_loc && w && alpha && delta_w && local_iters >= 0, COCOA_E_ARG,
+            "cocoa_local_sdca: bad argument");
+    const int64_t p0 = ctx->h_part_ptr[(size_t)part], p1 = ctx->h_part_ptr[(size_t)part + 1];
+    const int32_t nl = (int32_t)(p1 - p0);
+    if (local_iters >= 1) require(nl >= 1, COCOA_E_ARG, "IllegalArgumentException: empty partition");
+    const int64_t d = ctx->d;
+    hipStream_t s = ctx->stream;
+    // a one-partition problem over the loaded CSR
+    cocoa_ctx& c = *ctx;
+    const int saved_method = c.method;
+    c.method = plus ? COCOA_METHOD_COCOA_PLUS : COCOA_METHOD_COCOA;
+    const int32_t saved_max = c.max_nl;
+    c.max_nl = nl;
+    plan_solver(&c);
+    c.max_nl = saved_max;
+    c.method = saved_method;
+    DevBuf pp, smp, dwb, wb, wl, al, alw, sumb;
+    const int64_t h_pp[2] = {p0, p1};
+    upload(pp, h_pp, sizeof(h_pp), s);
+    smp.alloc(sizeof(int32_t) * (size_t)std::max(local_iters, 1));
+    dwb.alloc_zero(sizeof(double) * (size_t)d, s);
+    upload(wb, w, sizeof(double) * (size_t)d, s);
+    if (!plus) wl.alloc(sizeof(double) * (size_t)d);
+    al.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(ctx->tr.n, 1), s);
+    alw.alloc(sizeof(double) * (size_t)std::max<int64_t>(ctx->tr.n, 1));
+    if (nl) HIPCHK(hipMemcpyAsync(al.as<double>() + p0, alpha, sizeof(double) * (size_t)nl, hipMemcpyHostToDevice, s));
+    sumb.alloc(sizeof(double) * (size_t)d);
+    SolverArgs a = c.sa;
+    a.row_ptr = ctx->tr.row_ptr.as<int64_t>();
+    a.col = ctx->tr.col.as<int32_t>();
+    a.val = ctx->tr.val.as<double>();
+    a.y = ctx->tr.y.as<double>();
+    a.sqn = ctx->sqn.as<double>();
+    a.rowflags = ctx->rowflags.as<uint8_t>();
+    a.part_ptr = pp.as<int64_t>();
+    a.samples = smp.as<int32_t>();
+    a.alpha = al.as<double>();
+    a.alpha_work = alw.as<double>();
+    a.w = wb.as<double>();
+    a.dw = dwb.as<double>();
+    a.wloc = plus ? nullptr : wl.as<double>();
+    a.d = d;
+    a.H = local_iters;
+    a.any_dup = ctx->any_dup ? 1 : 0;
+    a.raw_alpha = 1;
+    a.lam_n = lambda * (double)n;
+    a.sigma = sigma;
+    a.scaling = 1.0;
+    if (local_iters >= 1) {
+        launch_sampler(pp.as<int64_t>(), 1, seed, local_iters, smp.as<int32_t>(), ctx->jump.as<uint64_t>(), s);
+        if (ctx->strict)
+            launch_solver_strict(plus ? MODE_PLUS : MODE_COCOA, c.vec_lds, c.alpha_lds, a, 1, c.lds_bytes, s);
+        else
+            launch_solver_fast(plus ? MODE_PLUS : MODE_COCOA, c.vec_lds, c.alpha_lds, a, 1, c.lds_bytes, s);
+        HIPCHK(hipGetLastError());
+    }
+    launch_fold(dwb.as<double>(), 1, d, sumb.as<double>(), nullptr, 1.0, false, s);
+    HIPCHK(hipGetLastError());
+    std::vector<double> old(alpha, alpha + nl);
+    HIPCHK(hipMemcpyAsync(delta_w, sumb.p, sizeof(double) * (size_t)d, hipMemcpyDeviceToHost, s));
+    if (nl) HIPCHK(hipMemcpyAsync(alpha, al.as<double>() + p0, sizeof(double) * (size_t)nl, hipMemcpyDeviceToHost, s));
+    if (!plus) HIPCHK(hipMemcpyAsync(w, wl.p, sizeof(double) * (size_t)d, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (delta_alpha)
+        for (int32_t i = 0; i < nl; ++i) delta_alpha[i] = alpha[i] - old[(size_t)i];  // CoCoA.scala:190
+    if (ctx->inited) plan_solver(ctx);
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_samples(cocoa_ctx* ctx, int32_t part, int32_t seed_plus_t, int32_t count, int32_t* out) {
+    CAPI_BEGIN(ctx)
+    require(part >= 0 && part < ctx->K_loc && count >= 0 && out, COCOA_E_ARG, "cocoa_samples: bad argument");
+    const int64_t h_pp[2] = {ctx->h_part_ptr[(size_t)part], ctx->h_part_ptr[(size_t)part + 1]};
+    require(h_pp[1] > h_pp[0], COCOA_E_ARG, "IllegalArgumentException: empty partition");
+    DevBuf pp, smp;
+    upload(pp, h_pp, sizeof(h_pp), ctx->stream);
+    smp.alloc(sizeof(int32_t) * (size_t)std::max(count, 1));
+    if (count) {
+        launch_sampler(pp.as<int64_t>(), 1, seed_plus_t, count, smp.as<int32_t>(), ctx->jump.as<uint64_t>(), ctx->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(out, smp.p, sizeof(int32_t) * (size_t)count, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    CAPI_END(ctx)
+}
+
+// ------------------------------------------------------------- profiling --
+extern "C" int cocoa_stats_enable(cocoa_ctx* ctx, int enable) {
+    CAPI_BEGIN(ctx)
+    ctx->drain();
+    ctx->stats = enable != 0;
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_kernel_stats(cocoa_ctx* ctx, int kernel, double* total_ms, int64_t* launches) {
+    CAPI_BEGIN(ctx)
+    require(kernel >= 0 && kernel < COCOA_K_COUNT, COCOA_E_ARG, "bad kernel id");
+    ctx->drain();
+    if (total_ms) *total_ms = ctx->tot_ms[kernel];
+    if (launches) *launches = ctx->cnt[kernel];
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_stats_reset(cocoa_ctx* ctx) {
+    CAPI_BEGIN(ctx)
+    ctx->drain();
+    for (int i = 0; i < COCOA_K_COUNT; ++i) ctx->tot_ms[i] = 0, ctx->cnt[i] = 0;
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
+    CAPI_BEGIN(ctx)
+    require(buf && len > 0, COCOA_E_ARG, "bad buffer");
+    std::snprintf(buf, (size_t)len,
+                  "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
+                  "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d}",
+                  ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
+                  ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl);
+    CAPI_END(ctx)
+}

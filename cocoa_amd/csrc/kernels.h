@@ -1,0 +1,110 @@
+// Kernel argument blocks and launcher declarations shared by the engine and
+// the two kernel translation units:
+//   kernels_fast.hip   -- compiled with -ffp-contract=fast (fast mode)
+//   kernels_strict.hip -- compiled with -ffp-contract=off  (bit-exact mode,
+//                          plus the fold/apply/sampler/strict-eval kernels)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace cocoa {
+
+enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2 };
+
+constexpr int kWave = 64;
+constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
+constexpr int kRegChunks = 4;       // rows with z <= 256 keep (col,val,vec) in registers
+
+// Per-batch step metadata, staged by the loader wave in LDS (SoA).
+struct BatchMeta {
+    int32_t r[kMetaSteps];     // row index within the partition (the sample)
+    int32_t off[kMetaSteps];   // offset of the row in the staged stream, -1 = read from HBM
+    int32_t z[kMetaSteps];     // nnz of the row
+    int32_t flags[kMetaSteps]; // bit0: row has duplicate column indices
+    int64_t beg[kMetaSteps];   // global entry offset of the row
+    double y[kMetaSteps];      // label
+    double q[kMetaSteps];      // Math.pow(norm(x), 2)
+    double xw[kMetaSteps];     // x . w (read-only w: CoCoA+ and MbCD), summed in stored order
+    int32_t m;                 // steps in this batch (0 = no more work)
+    int32_t pad[3];
+};
+
+struct SolverArgs {
+    const int64_t* row_ptr;   // rank-local CSR
+    const int32_t* col;
+    const double* val;
+    const double* y;
+    const double* sqn;        // per-row Math.pow(norm(x),2)
+    const uint8_t* rowflags;  // per-row flags (duplicates), may be null
+    const int64_t* part_ptr;  // K_loc + 1 row offsets
+    const int32_t* samples;   // K_loc * H
+    double* alpha;            // persistent alpha (rank-local rows)
+    double* alpha_work;       // working alpha copy when not in LDS
+    const double* w;          // shared w (read-only during the round)
+    double* dw;               // K_loc * d private deltaW (zero on entry)
+    double* wloc;             // K_loc * d task copy of w (CoCoA) when not in LDS
+    int64_t d;
+    int32_t H;
+    int32_t stream_cap;       // staged entries per batch buffer
+    int32_t any_dup;
+    int32_t raw_alpha;        // 1: write the raw local alpha (unit localSDCA API)
+    double lam_n;             // lambda * n
+    double sigma;             // sigma' = K * gamma (CoCoA+)
+    double scaling;           // alpha <- alphaOld + dAlpha * scaling
+    // LDS carve (byte offsets into dynamic LDS)
+    int32_t lds_stream_col[2];
+    int32_t lds_stream_val[2];
+    int32_t lds_meta[2];
+    int32_t lds_prod;         // loader scratch: stream_cap doubles
+    int32_t lds_scratch;      // compute scratch: kRegChunks*64 doubles
+    int32_t lds_vec;          // d doubles (deltaW, or w_loc for CoCoA) if VEC_LDS
+    int32_t lds_alpha;        // rows-of-largest-partition doubles if ALPHA_LDS
+};
+
+struct EvalArgs {
+    // train side
+    const int64_t* row_ptr;
+    const int32_t* col;
+    const double* val;
+    const double* y;
+    const double* alpha;
+    int64_t n;
+    // test side
+    const int64_t* t_row_ptr;
+    const int32_t* t_col;
+    const double* t_val;
+    const double* t_y;
+    int64_t n_test;
+    const double* w;
+    int64_t d;
+    // partitions (strict fold order)
+    const int64_t* part_ptr;
+    int32_t K;
+    int32_t pad;
+    // outputs
+    double* partials;         // [blocks][4] fast; per-row scratch strict
+    double* out;              // [4]: hinge_sum, alpha_sum, w_sq(norm^2 via sqrt), test_err_count
+    double* row_scratch;      // n doubles (strict)
+};
+
+// fast translation unit
+void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
+                        hipStream_t s);
+void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
+int eval_fast_blocks(int64_t n, int64_t n_test);
+
+// strict translation unit
+void launch_solver_strict(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
+                          hipStream_t s);
+void launch_eval_strict(const EvalArgs& a, hipStream_t s);
+void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H, int32_t* samples,
+                    const uint64_t* jump_tab, hipStream_t s);
+void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
+                 hipStream_t s);
+void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, hipStream_t s);
+void launch_scale(double* w, int64_t d, double scale, hipStream_t s);
+void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, double* out, hipStream_t s);
+void launch_sgd(bool local, const SolverArgs& a, double lambda, double t0, int grid, hipStream_t s);
+
+}  // namespace cocoa

@@ -1,0 +1,235 @@
+// Strict translation unit: compiled with -ffp-contract=off so that every
+// multiply and add rounds exactly like the JVM reference (no FMA).  Holds the
+// bit-exact local solver instantiations and every kernel whose result feeds
+// the shared state (sampler, deltaW fold, w apply, strict evaluation, SGD).
+#include "jrandom.h"
+#include "kernels.h"
+#include "solver_impl.h"
+#include "wave.h"
+
+namespace cocoa {
+
+void launch_solver_strict(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
+                          hipStream_t s) {
+    launch_solver_impl<true>(mode, vec_lds, alpha_lds, a, grid, lds, s);
+}
+
+// ---------------------------------------------------------------- sampler --
+// Partition k draws java.util.Random(seed).nextInt(n_k) H times
+// (CoCoA.scala:144,151).  Thread t of the block produces raw draw number
+// 256*c + t + 1 through the affine jump table; accepted draws are compacted
+// in order (a rejected raw value is skipped exactly as nextInt's loop does).
+// jt[2*(j-1)], jt[2*(j-1)+1] = (A_j, C_j) for j = 1..256.
+__global__ __launch_bounds__(256) void sampler_kernel(const int64_t* part_ptr, int32_t seed, int32_t H,
+                                                      int32_t* samples, const uint64_t* jt) {
+    __shared__ int32_t wtot[4];
+    const int k = blockIdx.x;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wv = t >> 6;
+    const int32_t bound = (int32_t)(part_ptr[k + 1] - part_ptr[k]);
+    int32_t* out = samples + (size_t)k * H;
+    if (bound <= 0) return;
+    const uint64_t s0 = jr_scramble((int64_t)seed);
+    uint64_t st = (jt[2 * t] * s0 + jt[2 * t + 1]) & kJrMask;
+    const uint64_t A256 = jt[2 * 255], C256 = jt[2 * 255 + 1];
+    int32_t base = 0;
+    while (base < H) {
+        int32_t v;
+        const bool acc = jr_accept(jr_bits31(st), bound, &v);
+        const uint64_t bal = __ballot(acc);
+        const int32_t pre = (int32_t)__popcll(bal & ((1ULL << lane) - 1ULL));
+        if (lane == 0) wtot[wv] = (int32_t)__popcll(bal);
+        __syncthreads();
+        int32_t off = 0, tot = 0;
+        for (int i = 0; i < 4; ++i) {
+            if (i < wv) off += wtot[i];
+            tot += wtot[i];
+        }
+        const int32_t pos = base + off + pre;
+        if (acc && pos < H) out[pos] = v;
+        base += tot;
+        st = (A256 * st + C256) & kJrMask;
+        __syncthreads();
+    }
+}
+
+void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H, int32_t* samples,
+                    const uint64_t* jump_tab, hipStream_t s) {
+    sampler_kernel<<<K, 256, 0, s>>>(part_ptr, seed, H, samples, jump_tab);
+}
+
+// ------------------------------------------------------- deltaW fold/apply --
+// sum = ((dW_0 + dW_1) + dW_2) + ... in partition order (the reference's
+// reduce(_ + _), CoCoA.scala:47), zeroing each private slice for the next
+// round; then w += sum * mult (CoCoA.scala:48) or the sum is stored for an
+// external all-reduce.
+__global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_t d, double* dw_sum, double* w,
+                                                   double mult, int apply) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
+        double s = dw[j];
+        dw[j] = 0.0;
+        for (int32_t k = 1; k < K; ++k) {
+            const size_t o = (size_t)k * d + j;
+            s = s + dw[o];
+            dw[o] = 0.0;
+        }
+        if (apply)
+            w[j] = w[j] + (s * mult);
+        else
+            dw_sum[j] = s;
+    }
+}
+
+void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
+                 hipStream_t s) {
+    int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
+    if (blocks < 1) blocks = 1;
+    fold_kernel<<<blocks, 256, 0, s>>>(const_cast<double*>(dw), K, d, dw_sum, w, mult, apply ? 1 : 0);
+}
+
+__global__ __launch_bounds__(256) void apply_kernel(double* w, const double* dw_sum, int64_t d, double mult) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x)
+        w[j] = w[j] + (dw_sum[j] * mult);
+}
+
+void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, hipStream_t s) {
+    int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
+    apply_kernel<<<blocks < 1 ? 1 : blocks, 256, 0, s>>>(w, dw_sum, d, mult);
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(double* w, int64_t d, double scale) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x)
+        w[j] = w[j] * scale;  // w :*= scale (SGD.scala:298)
+}
+
+void launch_scale(double* w, int64_t d, double scale, hipStream_t s) {
+    int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
+    scale_kernel<<<blocks < 1 ? 1 : blocks, 256, 0, s>>>(w, d, scale);
+}
+
+// ------------------------------------------------------------ strict eval --
+// Pass 1: one lane per row, dot in stored order; train rows store their hinge
+// loss, test rows store 1.0 for a misclassification (OptUtils.scala:57-61,95-98).
+__global__ __launch_bounds__(256) void eval_rows_strict(EvalArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n) {
+        const int64_t b = a.row_ptr[i], e = a.row_ptr[i + 1];
+        double s = 0.0;
+        for (int64_t q = b; q < e; ++q) s += a.val[q] * a.w[a.col[q]];
+        a.row_scratch[i] = jmax(1 - a.y[i] * (s), 0.0);
+    } else if (i < a.n + a.n_test) {
+        const int64_t r = i - a.n;
+        const int64_t b = a.t_row_ptr[r], e = a.t_row_ptr[r + 1];
+        double s = 0.0;
+        for (int64_t q = b; q < e; ++q) s += a.t_val[q] * a.w[a.t_col[q]];
+        a.row_scratch[i] = ((s) * (a.t_y[r]) > 0) ? 0.0 : 1.0;
+    }
+}
+
+// Pass 2: per-partition reduceLeft of the hinge losses and DenseVector.sum of
+// alpha (thread k), merged in partition order; ||w||^2 summed in index order.
+__global__ __launch_bounds__(1024) void eval_fold_strict(EvalArgs a) {
+    double* part = a.partials;  // [K][2]
+    for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
+        const int64_t r0 = a.part_ptr[k], r1 = a.part_ptr[k + 1];
+        double h = 0.0, al = 0.0;
+        for (int64_t r = r0; r < r1; ++r) {
+            h = (r == r0) ? a.row_scratch[r] : h + a.row_scratch[r];
+            al += a.alpha[r];
+        }
+        part[2 * k] = h;
+        part[2 * k + 1] = al;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double h = 0.0, al = 0.0;
+        bool have = false;
+        for (int32_t q = 0; q < a.K; ++q) {
+            al = (q == 0) ? part[2 * q + 1] : al + part[2 * q + 1];
+            if (a.part_ptr[q + 1] > a.part_ptr[q]) {
+                h = have ? h + part[2 * q] : part[2 * q];
+                have = true;
+            }
+        }
+        double w2 = 0.0;
+        for (int64_t j = 0; j < a.d; ++j) w2 += a.w[j] * a.w[j];
+        double err = 0.0;
+        for (int64_t r = 0; r < a.n_test; ++r) err += a.row_scratch[a.n + r];
+        a.out[0] = h;
+        a.out[1] = al;
+        a.out[2] = w2;
+        a.out[3] = err;
+    }
+}
+
+void launch_eval_strict(const EvalArgs& a, hipStream_t s) {
+    const int64_t rows = a.n + a.n_test;
+    const int blocks = (int)((rows + 255) / 256);
+    if (blocks > 0) eval_rows_strict<<<blocks, 256, 0, s>>>(a);
+    eval_fold_strict<<<1, 1024, 0, s>>>(a);
+}
+
+// -------------------------------------------------------------- SGD (C5) --
+// SGD.partitionUpdate (SGD.scala:336-388), one workgroup per partition.
+// mb-SGD: w is the driver's (already shrunk) w, read-only; deltaW accumulates
+// x*y over violators.  local-SGD: the task's copy w_loc is shrunk by
+// (1 - step*lambda) every step (O(d), as the reference does) and moved by
+// x*y*step; the returned deltaW is w_loc - wInit.
+template <bool LOCAL>
+__global__ __launch_bounds__(256) void sgd_kernel(SolverArgs a, double lambda, double t0) {
+    __shared__ double red[4];
+    __shared__ double sh_eval;
+    const int k = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t p0 = a.part_ptr[k];
+    const int64_t d = a.d;
+    double* dwk = a.dw + (size_t)k * d;
+    double* wl = LOCAL ? a.wloc + (size_t)k * d : const_cast<double*>(a.w);
+    if (LOCAL) {
+        for (int64_t j = tid; j < d; j += 256) wl[j] = a.w[j];
+        __syncthreads();
+    }
+    for (int32_t i = 1; i <= a.H; ++i) {
+        const double step = 1.0 / (lambda * (t0 + (double)i));         // SGD.scala:355
+        const int32_t idx = a.samples[(size_t)k * a.H + (i - 1)];
+        const int64_t gr = p0 + idx;
+        const int64_t b = a.row_ptr[gr], e = a.row_ptr[gr + 1];
+        const double yv = a.y[gr];
+        if (wv == 0) {
+            // x.dot(w) in stored order (strict: lane 0 sequential)
+            double s = 0.0;
+            if (lane == 0)
+                for (int64_t q = b; q < e; ++q) s += a.val[q] * wl[a.col[q]];
+            if (lane == 0) sh_eval = 1.0 - (yv * (s));                    // SGD.scala:364
+        }
+        __syncthreads();
+        const double ev = sh_eval;
+        if (LOCAL) {
+            const double scale = 1.0 - (step * lambda);                  // SGD.scala:368-369
+            for (int64_t j = tid; j < d; j += 256) wl[j] = wl[j] * scale;
+            __syncthreads();
+        }
+        if (ev > 0) {                                                    // SGD.scala:373-379
+            if (tid == 0) {
+                for (int64_t q = b; q < e; ++q) {
+                    const double u = a.val[q] * yv;
+                    if (!LOCAL) dwk[a.col[q]] = dwk[a.col[q]] + u;
+                    if (LOCAL) wl[a.col[q]] = wl[a.col[q]] + (u * step);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (LOCAL)
+        for (int64_t j = tid; j < d; j += 256) dwk[j] = wl[j] - a.w[j];  // deltaW = w - wInit (SGD.scala:382)
+    (void)red;
+}
+
+void launch_sgd(bool local, const SolverArgs& a, double lambda, double t0, int grid, hipStream_t s) {
+    if (local)
+        sgd_kernel<true><<<grid, 256, 0, s>>>(a, lambda, t0);
+    else
+        sgd_kernel<false><<<grid, 256, 0, s>>>(a, lambda, t0);
+}
+
+}  // namespace cocoa

@@ -1,0 +1,373 @@
+// Local-solver kernel template: one workgroup per partition, two waves.
+//
+//   wave 1 = loader: runs one batch ahead.  For up to 64 upcoming coordinate
+//            steps it reads the sample indices, the rows' metadata and their
+//            (col,val) entries from HBM into an LDS stream buffer, and -- when
+//            w is read-only during the round (CoCoA+, MbCD) -- also the dot
+//            x_i.w in stored-entry order.
+//   wave 0 = solver: the strictly sequential chain of H coordinate steps of
+//            CoCoA.localSDCA (CoCoA.scala:148-188) / MinibatchCD
+//            (MinibatchCD.scala:210-240), reading its rows from LDS.  The only
+//            memory it waits on per step is the gather of the mutable vector
+//            (deltaW for CoCoA+, the task's w copy for CoCoA), which lives in
+//            LDS when d fits, else in a private HBM/L2 slice.
+//
+// Double-buffered batches, one workgroup barrier per batch.  STRICT selects
+// the bit-exact arithmetic (sequential dot sums in stored order by lane 0, no
+// FMA: this header is compiled with -ffp-contract=off in kernels_strict.hip);
+// otherwise wave-tree (DPP) sums and fused multiply-adds.
+#pragma once
+#include "kernels.h"
+#include "wave.h"
+
+namespace cocoa {
+
+constexpr int kLoadUnroll = 8;  // 64-entry units each loader iteration keeps in flight
+
+__device__ __forceinline__ int find_step(int32_t p, int32_t excl, int m) {
+    // largest j < m with excl_j <= p (excl held by lane j); all lanes active
+    int lo = 0;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+        const int c = lo + st;
+        const int32_t e = __shfl(excl, c < 64 ? c : 63, 64);
+        if (c < m && e <= p) lo = c;
+    }
+    return lo;
+}
+
+template <int MODE, bool STRICT>
+__device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& cursor, BatchMeta* mb, int32_t* scol,
+                           double* sval, double* prod) {
+    const int lane = lane_id();
+    const int32_t H = a.H;
+    const int32_t C = a.stream_cap;
+    if (cursor >= H) {
+        if (lane == 0) mb->m = 0;
+        return;
+    }
+    const int32_t s = cursor + lane;
+    const bool valid = s < H;
+    int32_t idx = 0;
+    int64_t beg = 0, z = 0;
+    double yv = 0.0, qv = 0.0;
+    int32_t fl = 0;
+    if (valid) {
+        idx = a.samples[(size_t)k * H + s];
+        const int64_t gr = p0 + idx;
+        beg = a.row_ptr[gr];
+        z = a.row_ptr[gr + 1] - beg;
+        yv = a.y[gr];
+        qv = a.sqn[gr];
+        if (a.any_dup) fl = a.rowflags[gr];
+    }
+    const bool staged = z <= C;
+    const int32_t zz = (valid && staged) ? (int32_t)z : 0;
+    const int32_t incl = wave_incl_scan(zz);
+    const bool fits = valid && incl <= C;
+    const uint64_t mask = __ballot(fits);
+    const int m = (~mask == 0ULL) ? 64 : __builtin_ctzll(~mask);  // >= 1: step `cursor` always fits
+    const int32_t excl = incl - zz;
+    if (lane < m) {
+        mb->r[lane] = idx;
+        mb->off[lane] = staged ? excl : -1;
+        mb->z[lane] = (int32_t)z;
+        mb->flags[lane] = fl;
+        mb->beg[lane] = beg;
+        mb->y[lane] = yv;
+        mb->q[lane] = qv;
+    }
+    const int32_t T = __shfl(incl, m - 1, 64);
+    // stream the batch's entries: 64 consecutive packed positions per unit
+    for (int32_t base = 0; base < T; base += 64 * kLoadUnroll) {
+        int32_t pc[kLoadUnroll];
+        double pv[kLoadUnroll], pw[kLoadUnroll];
+#pragma unroll
+        for (int u = 0; u < kLoadUnroll; ++u) {
+            const int32_t p = base + 64 * u + lane;
+            const int32_t pq = p < T ? p : T - 1;
+            const int j = find_step(pq, excl, m);
+            const int64_t bj = __shfl(beg, j, 64);
+            const int32_t ej = __shfl(excl, j, 64);
+            pc[u] = 0;
+            pv[u] = 0.0;
+            if (p < T) {
+                const int64_t e = bj + (pq - ej);
+                pc[u] = a.col[e];
+                pv[u] = a.val[e];
+            }
+        }
+        if (MODE != MODE_COCOA) {
+#pragma unroll
+            for (int u = 0; u < kLoadUnroll; ++u) {
+                const int32_t p = base + 64 * u + lane;
+                pw[u] = p < T ? a.w[pc[u]] : 0.0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kLoadUnroll; ++u) {
+            const int32_t p = base + 64 * u + lane;
+            if (p < T) {
+                scol[p] = pc[u];
+                sval[p] = pv[u];
+                if (MODE != MODE_COCOA) prod[p] = pv[u] * pw[u];
+            }
+        }
+    }
+    if (MODE != MODE_COCOA) {
+        wave_lds_sync();
+        // x.w for each step, one lane per step, summed in stored-entry order
+        double xw = 0.0;
+        if (lane < m) {
+            if (staged) {
+                for (int32_t q = 0; q < (int32_t)z; ++q) xw += prod[excl + q];
+            } else {
+                for (int64_t q = 0; q < z; ++q) xw += a.val[beg + q] * a.w[a.col[beg + q]];
+            }
+            mb->xw[lane] = xw;
+        }
+    }
+    if (lane == 0) mb->m = m;
+    cursor += m;
+}
+
+// Sequential (strict) or tree (fast) sum of the products held in registers.
+template <bool STRICT>
+__device__ __forceinline__ double dot_regs(const double (&prod)[kRegChunks], int32_t z, double* scratch) {
+    const int lane = lane_id();
+    if (STRICT) {
+#pragma unroll
+        for (int u = 0; u < kRegChunks; ++u)
+            if (lane + 64 * u < z) scratch[lane + 64 * u] = prod[u];
+        wave_lds_sync();
+        double t = 0.0;
+        if (lane == 0)
+            for (int32_t q = 0; q < z; ++q) t += scratch[q];
+        t = uni(t);
+        wave_lds_sync();
+        return t;
+    } else {
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < kRegChunks; ++u) acc += prod[u];
+        return wave_sum(acc);
+    }
+}
+
+template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS>
+__device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const int32_t* scol, const double* sval,
+                              double* scratch, double* vec, double* dwk, double* alv) {
+    const int lane = lane_id();
+    const int m = uni(mb->m);
+    const double lam_n = a.lam_n;
+    const double sigma = a.sigma;
+    for (int s = 0; s < m; ++s) {
+        const int32_t r = uni(mb->r[s]);
+        const int32_t off = uni(mb->off[s]);
+        const int32_t z = uni(mb->z[s]);
+        const int32_t fl = uni(mb->flags[s]);
+        const double yv = uni(mb->y[s]);
+        const double qv = uni(mb->q[s]);
+        const double xw = MODE != MODE_COCOA ? uni(mb->xw[s]) : 0.0;
+        const double aa = uni(alv[r]);  // after the previous step's write (in order)
+
+        const bool fast_path = off >= 0 && z <= 64 * kRegChunks && (fl & 1) == 0;
+        int32_t pc[kRegChunks];
+        double pv[kRegChunks], pd[kRegChunks];
+        double sdot = 0.0;
+        if (fast_path) {
+#pragma unroll
+            for (int u = 0; u < kRegChunks; ++u) {
+                const int32_t p = lane + 64 * u;
+                pc[u] = 0;
+                pv[u] = 0.0;
+                pd[u] = 0.0;
+                if (p < z) {
+                    pc[u] = scol[off + p];
+                    pv[u] = sval[off + p];
+                    if (MODE != MODE_MBCD) pd[u] = vec[pc[u]];
+                }
+            }
+            if (MODE != MODE_MBCD) {
+                double prod[kRegChunks];
+#pragma unroll
+                for (int u = 0; u < kRegChunks; ++u) prod[u] = pv[u] * pd[u];
+                sdot = dot_regs<STRICT>(prod, z, scratch);
+            }
+        } else if (MODE != MODE_MBCD) {
+            // generic path: long / unstaged / duplicate-column rows
+            const int32_t* sc = off >= 0 ? scol + off : a.col + uni(mb->beg[s]);
+            const double* sv = off >= 0 ? sval + off : a.val + uni(mb->beg[s]);
+            if (STRICT) {
+                double t = 0.0;
+                for (int32_t c0 = 0; c0 < z; c0 += 64) {
+                    const int32_t p = c0 + lane;
+                    if (p < z) scratch[lane] = sv[p] * vec[sc[p]];
+                    wave_lds_sync();
+                    const int32_t cnt = z - c0 < 64 ? z - c0 : 64;
+                    if (lane == 0)
+                        for (int32_t q = 0; q < cnt; ++q) t += scratch[q];
+                    wave_lds_sync();
+                }
+                sdot = uni(t);
+            } else {
+                double acc = 0.0;
+                for (int32_t p = lane; p < z; p += 64) acc += sv[p] * vec[sc[p]];
+                sdot = wave_sum(acc);
+            }
+        }
+
+        double grad;
+        if (MODE == MODE_PLUS)
+            grad = (yv * (xw + (sigma * sdot)) - 1.0) * lam_n;   // CoCoA.scala:159
+        else if (MODE == MODE_COCOA)
+            grad = (yv * (sdot) - 1.0) * lam_n;                  // CoCoA.scala:161
+        else
+            grad = (yv * (xw) - 1.0) * lam_n;                    // MinibatchCD.scala:219
+        double proj = grad;                                      // CoCoA.scala:166-170
+        if (aa <= 0.0)
+            proj = jmin(grad, 0.0);
+        else if (aa >= 1.0)
+            proj = jmax(grad, 0.0);
+        if (fabs(proj) != 0.0) {                                 // CoCoA.scala:172
+            const double qii = MODE == MODE_PLUS ? qv * sigma : qv;
+            double na = 1.0;
+            if (qii != 0.0) na = jmin(jmax((aa - (grad / qii)), 0.0), 1.0);
+            const double coef = (yv * (na - aa)) / lam_n;        // CoCoA.scala:181
+            if (fast_path) {
+#pragma unroll
+                for (int u = 0; u < kRegChunks; ++u) {
+                    if (lane + 64 * u < z) {
+                        const double upd = pv[u] * coef;
+                        if (MODE == MODE_PLUS) {
+                            vec[pc[u]] = pd[u] + upd;                  // deltaW += update
+                        } else if (MODE == MODE_COCOA) {
+                            vec[pc[u]] = pd[u] + upd;                  // w += update
+                            if (STRICT) dwk[pc[u]] = dwk[pc[u]] + upd; // deltaW += update
+                            else unsafeAtomicAdd(dwk + pc[u], upd);
+                        } else {
+                            if (STRICT) vec[pc[u]] = vec[pc[u]] + upd;
+                            else if (VEC_LDS) atomicAdd(vec + pc[u], upd);
+                            else unsafeAtomicAdd(vec + pc[u], upd);
+                        }
+                    }
+                }
+            } else {
+                const int32_t* sc = off >= 0 ? scol + off : a.col + uni(mb->beg[s]);
+                const double* sv = off >= 0 ? sval + off : a.val + uni(mb->beg[s]);
+                if (fl & 1) {
+                    // duplicate column indices: the reference's sequential scatter
+                    if (lane == 0) {
+                        for (int32_t q = 0; q < z; ++q) {
+                            const int32_t c = sc[q];
+                            const double upd = sv[q] * coef;
+                            vec[c] = vec[c] + upd;
+                            if (MODE == MODE_COCOA) dwk[c] = dwk[c] + upd;
+                        }
+                    }
+                } else {
+                    for (int32_t p = lane; p < z; p += 64) {
+                        const int32_t c = sc[p];
+                        const double upd = sv[p] * coef;
+                        vec[c] = vec[c] + upd;
+                        if (MODE == MODE_COCOA) {
+                            if (STRICT) dwk[c] = dwk[c] + upd;
+                            else unsafeAtomicAdd(dwk + c, upd);
+                        }
+                    }
+                }
+            }
+            if (lane == 0) alv[r] = na;                          // CoCoA.scala:186
+        }
+    }
+}
+
+template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS>
+__global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int k = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int64_t p0 = a.part_ptr[k], p1 = a.part_ptr[k + 1];
+    const int32_t nl = (int32_t)(p1 - p0);
+    const int64_t d = a.d;
+    double* dwk = a.dw + (size_t)k * d;
+    double* vec;
+    if (VEC_LDS)
+        vec = (double*)(lds + a.lds_vec);
+    else
+        vec = MODE == MODE_COCOA ? a.wloc + (size_t)k * d : dwk;
+    double* alv = ALPHA_LDS ? (double*)(lds + a.lds_alpha) : a.alpha_work + p0;
+    double* scratch = (double*)(lds + a.lds_scratch);
+    double* prod = (double*)(lds + a.lds_prod);
+
+    // prologue: alphaOld stays in a.alpha; the working copy is alv
+    for (int32_t i = tid; i < nl; i += 128) alv[i] = a.alpha[p0 + i];
+    if (VEC_LDS) {
+        for (int64_t j = tid; j < d; j += 128) vec[j] = MODE == MODE_COCOA ? a.w[j] : 0.0;
+    } else if (MODE == MODE_COCOA) {
+        for (int64_t j = tid; j < d; j += 128) vec[j] = a.w[j];  // the task's private copy of w
+    }
+    int32_t cursor = 0;
+    if (wave == 1)
+        load_batch<MODE, STRICT>(a, k, p0, cursor, (BatchMeta*)(lds + a.lds_meta[0]), (int32_t*)(lds + a.lds_stream_col[0]),
+                                 (double*)(lds + a.lds_stream_val[0]), prod);
+    __syncthreads();
+    for (int b = 0;; ++b) {
+        const int cur = b & 1;
+        const BatchMeta* mb = (const BatchMeta*)(lds + a.lds_meta[cur]);
+        if (mb->m == 0) break;
+        if (wave == 1) {
+            load_batch<MODE, STRICT>(a, k, p0, cursor, (BatchMeta*)(lds + a.lds_meta[cur ^ 1]),
+                                     (int32_t*)(lds + a.lds_stream_col[cur ^ 1]), (double*)(lds + a.lds_stream_val[cur ^ 1]),
+                                     prod);
+        } else {
+            compute_batch<MODE, STRICT, VEC_LDS, ALPHA_LDS>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
+                                                            (const double*)(lds + a.lds_stream_val[cur]), scratch, vec,
+                                                            dwk, alv);
+        }
+        __syncthreads();
+    }
+    // epilogue: alpha = alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101,
+    // MinibatchCD.scala:242-243)
+    if (a.raw_alpha) {
+        for (int32_t i = tid; i < nl; i += 128) a.alpha[p0 + i] = alv[i];
+        if (VEC_LDS && MODE == MODE_COCOA)
+            for (int64_t j = tid; j < d; j += 128) a.wloc[(size_t)k * d + j] = vec[j];
+    } else {
+        for (int32_t i = tid; i < nl; i += 128) {
+            const double old = a.alpha[p0 + i];
+            a.alpha[p0 + i] = old + ((alv[i] - old) * a.scaling);
+        }
+    }
+    if (VEC_LDS && MODE != MODE_COCOA)
+        for (int64_t j = tid; j < d; j += 128) dwk[j] = vec[j];
+}
+
+template <bool STRICT>
+void launch_solver_impl(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
+                        hipStream_t s) {
+#define COCOA_LAUNCH(M, V, A)                                                                        \
+    do {                                                                                             \
+        auto kern = solver_kernel<M, STRICT, V, A>;                                                  \
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+        kern<<<grid, 128, lds, s>>>(a);                                                              \
+    } while (0)
+#define COCOA_LAUNCH_M(M)                           \
+    do {                                            \
+        if (vec_lds && alpha_lds) COCOA_LAUNCH(M, true, true);   \
+        else if (vec_lds) COCOA_LAUNCH(M, true, false);          \
+        else if (alpha_lds) COCOA_LAUNCH(M, false, true);        \
+        else COCOA_LAUNCH(M, false, false);                      \
+    } while (0)
+    if (mode == MODE_PLUS)
+        COCOA_LAUNCH_M(MODE_PLUS);
+    else if (mode == MODE_COCOA)
+        COCOA_LAUNCH_M(MODE_COCOA);
+    else
+        COCOA_LAUNCH_M(MODE_MBCD);
+#undef COCOA_LAUNCH_M
+#undef COCOA_LAUNCH
+}
+
+}  // namespace cocoa

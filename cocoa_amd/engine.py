@@ -1,0 +1,158 @@
+"""Engine: one libcocoa_hip context (one GPU, one stream) holding one rank's
+partitions.  Thin, typed wrapper over include/cocoa_capi.h."""
+import ctypes
+import json
+
+import numpy as np
+
+from . import _capi as C
+
+
+class Engine:
+    def __init__(self, device=0, strict=False, stream=None):
+        """stream: a hipStream_t handle as int (e.g. torch.cuda.current_stream().cuda_stream)."""
+        h = ctypes.c_void_p()
+        C.check(C.lib().cocoa_create(int(device), 1 if strict else 0, ctypes.c_void_p(stream or 0), ctypes.byref(h)))
+        self.h = h
+        self.strict = strict
+        self.d = 0
+        self.n_rows = 0
+        self._keep = []
+
+    # -- data ----------------------------------------------------------------
+    def set_train(self, data, part_begin=0, num_parts_global=None):
+        data = data.contiguous()
+        K = data.num_parts
+        Kg = K if num_parts_global is None else num_parts_global
+        C.check(C.lib().cocoa_set_train(self.h, K, C.i64p(data.part_ptr), C.i64p(data.row_ptr), C.i32p(data.col),
+                                        C.f64p(data.val), C.f64p(data.y), data.n, data.num_features, part_begin, Kg),
+                self.h)
+        self.d = data.num_features
+        self.n_rows = data.n
+        self.K_loc, self.K_glob, self.part_begin = K, Kg, part_begin
+
+    def set_test(self, data):
+        data = data.contiguous()
+        C.check(C.lib().cocoa_set_test(self.h, C.i64p(data.row_ptr), C.i32p(data.col), C.f64p(data.val),
+                                       C.f64p(data.y), data.n), self.h)
+
+    # -- solver --------------------------------------------------------------
+    def init(self, method, n, num_rounds, local_iters, lam, beta=1.0, gamma=1.0, debug_iter=10, seed=0,
+             chkpt_iter=100, w_init=None):
+        self.params = C.Params(n, num_rounds, local_iters, 0, lam, beta, gamma)
+        self.debug = C.Debug(debug_iter, seed, chkpt_iter, 0)
+        wi = None if w_init is None else np.ascontiguousarray(w_init, np.float64)
+        C.check(C.lib().cocoa_init(self.h, ctypes.byref(self.params), ctypes.byref(self.debug),
+                                   C.METHODS[method] if isinstance(method, str) else int(method),
+                                   C.f64p(wi) if wi is not None else None), self.h)
+
+    def round(self, t):
+        C.check(C.lib().cocoa_round(self.h, t), self.h)
+
+    def round_local(self, t):
+        C.check(C.lib().cocoa_round_local(self.h, t), self.h)
+
+    def round_apply(self):
+        C.check(C.lib().cocoa_round_apply(self.h), self.h)
+
+    def dw_sum_ptr(self):
+        p = ctypes.c_void_p()
+        C.check(C.lib().cocoa_dw_sum_device_ptr(self.h, ctypes.byref(p)), self.h)
+        return p.value
+
+    def set_dw_sum_buffer(self, device_ptr):
+        C.check(C.lib().cocoa_set_dw_sum_buffer(self.h, ctypes.c_void_p(device_ptr or 0)), self.h)
+
+    def eval(self):
+        r = C.EvalResult()
+        C.check(C.lib().cocoa_eval(self.h, ctypes.byref(r)), self.h)
+        return r.as_dict()
+
+    def eval_finish(self, hinge_sum, alpha_sum, w_sq, err, test_rows):
+        r = C.EvalResult()
+        C.check(C.lib().cocoa_eval_finish(self.h, hinge_sum, alpha_sum, w_sq, int(err), int(test_rows),
+                                          ctypes.byref(r)), self.h)
+        return r.as_dict()
+
+    def run(self, method, n, num_rounds, local_iters, lam, beta=1.0, gamma=1.0, debug_iter=10, seed=0,
+            w_init=None, callback=None):
+        self.params = C.Params(n, num_rounds, local_iters, 0, lam, beta, gamma)
+        self.debug = C.Debug(debug_iter, seed, 100, 0)
+
+        def _cb(user, t, ev):
+            if callback is not None:
+                callback(t, ev.contents.as_dict())
+
+        cb = C.ROUND_CB(_cb)
+        wi = None if w_init is None else np.ascontiguousarray(w_init, np.float64)
+        C.check(C.lib().cocoa_run(self.h, ctypes.byref(self.params), ctypes.byref(self.debug),
+                                  C.METHODS[method] if isinstance(method, str) else int(method),
+                                  C.f64p(wi) if wi is not None else None, cb, None), self.h)
+
+    def w(self):
+        out = np.zeros(self.d, np.float64)
+        C.check(C.lib().cocoa_get_w(self.h, C.f64p(out)), self.h)
+        return out
+
+    def alpha(self):
+        out = np.zeros(self.n_rows, np.float64)
+        C.check(C.lib().cocoa_get_alpha(self.h, C.f64p(out)), self.h)
+        return out
+
+    def set_w(self, w):
+        w = np.ascontiguousarray(w, np.float64)
+        C.check(C.lib().cocoa_set_w(self.h, C.f64p(w)), self.h)
+
+    def set_alpha(self, a):
+        a = np.ascontiguousarray(a, np.float64)
+        C.check(C.lib().cocoa_set_alpha(self.h, C.f64p(a)), self.h)
+
+    def local_sdca(self, part, w, local_iters, lam, n, alpha, seed, plus, sigma):
+        """CoCoA.localSDCA on partition `part` (CoCoA.scala:130).  w and alpha are
+        updated in place like the reference; returns (deltaAlpha, deltaW)."""
+        assert w.dtype == np.float64 and alpha.dtype == np.float64
+        dw = np.zeros(self.d, np.float64)
+        da = np.zeros(len(alpha), np.float64)
+        C.check(C.lib().cocoa_local_sdca(self.h, part, C.f64p(w), local_iters, lam, n, C.f64p(alpha), seed,
+                                         1 if plus else 0, sigma, C.f64p(dw), C.f64p(da)), self.h)
+        return da, dw
+
+    def samples(self, part, seed_plus_t, count):
+        out = np.zeros(count, np.int32)
+        C.check(C.lib().cocoa_samples(self.h, part, seed_plus_t, count, C.i32p(out)), self.h)
+        return out
+
+    # -- profiling -----------------------------------------------------------
+    def stats_enable(self, on=True):
+        C.check(C.lib().cocoa_stats_enable(self.h, 1 if on else 0), self.h)
+
+    def stats_reset(self):
+        C.check(C.lib().cocoa_stats_reset(self.h), self.h)
+
+    def kernel_stats(self):
+        out = {}
+        for i, name in enumerate(C.KERNEL_NAMES):
+            ms = ctypes.c_double()
+            cnt = ctypes.c_int64()
+            C.check(C.lib().cocoa_kernel_stats(self.h, i, ctypes.byref(ms), ctypes.byref(cnt)), self.h)
+            out[name] = {"total_ms": ms.value, "launches": cnt.value}
+        return out
+
+    def plan(self):
+        buf = ctypes.create_string_buffer(1024)
+        C.check(C.lib().cocoa_plan_info(self.h, buf, 1024), self.h)
+        return json.loads(buf.value.decode())
+
+    def sync(self):
+        C.check(C.lib().cocoa_sync(self.h), self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            C.lib().cocoa_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,212 @@
+/*
+ * cocoa_capi.h -- C ABI of libcocoa_hip.so, the MI355X-native engine for the
+ * per-round CoCoA / CoCoA+ hot path of calvinmccarter/cocoa.
+ *
+ * Plain pointers and sizes only (no torch / HIP types).  Every function
+ * returns 0 on success or a negative COCOA_E_* code; the message of the last
+ * failure is available from cocoa_last_error(ctx) (or cocoa_last_error(NULL)
+ * for failures that happen before a context exists).
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the reference repository root).  How the unchanged
+ * Scala driver binds to these symbols (JNI / Panama FFM) is in INTEGRATION.md.
+ *
+ * Ownership: the caller owns every host buffer it passes; the engine copies
+ * inputs to device memory and copies results out.  A context owns its device
+ * memory and runs on one HIP device and one HIP stream; it is not thread-safe
+ * and is driven from one host thread.  Multi-GPU = one process (and one
+ * context) per GPU; the per-round deltaW exchange is done by the caller
+ * (RCCL via torch.distributed in cocoa_amd.dist) between
+ * cocoa_round_local() and cocoa_round_apply().
+ */
+#ifndef COCOA_CAPI_H
+#define COCOA_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COCOA_CAPI_VERSION 1
+
+/* error codes */
+#define COCOA_OK 0
+#define COCOA_E_ARG (-1)        /* IllegalArgumentException analogue       */
+#define COCOA_E_PARSE (-2)      /* NumberFormatException / MatchError       */
+#define COCOA_E_RANGE (-3)      /* ArrayIndexOutOfBounds (feature index)    */
+#define COCOA_E_IO (-4)         /* file not found / read error              */
+#define COCOA_E_HIP (-5)        /* HIP runtime error                        */
+#define COCOA_E_STATE (-6)      /* call out of order (no data, not inited)  */
+#define COCOA_E_NODEV (-7)      /* no HIP device / kernels not loadable     */
+
+/* methods: hingeDriver.scala:84-109 */
+#define COCOA_METHOD_COCOA_PLUS 0 /* CoCoA.runCoCoA(plus=true)   CoCoA.scala:22   */
+#define COCOA_METHOD_COCOA 1      /* CoCoA.runCoCoA(plus=false)  CoCoA.scala:22   */
+#define COCOA_METHOD_MBCD 2       /* MinibatchCD.runMbCD         MinibatchCD.scala:19 */
+#define COCOA_METHOD_MBSGD 3      /* SGD.runSGD(local=false)     SGD.scala:21     */
+#define COCOA_METHOD_LOCALSGD 4   /* SGD.runSGD(local=true)      SGD.scala:21     */
+
+/* Params (OptClasses.scala:21-29), minus the unused `loss` closure and with
+ * wInit passed separately (cocoa_init). */
+typedef struct {
+    int32_t n;           /* global number of examples (Params.n)            */
+    int32_t num_rounds;  /* T                                                 */
+    int32_t local_iters; /* H                                                 */
+    int32_t _pad;
+    double lambda;
+    double beta;         /* CoCoA scaling beta/K                              */
+    double gamma;        /* CoCoA+ aggregation gamma (sigma' = K*gamma)       */
+} cocoa_params;
+
+/* DebugParams (OptClasses.scala:38-42); testData is set with cocoa_set_test. */
+typedef struct {
+    int32_t debug_iter;  /* <= 0: no per-round evaluation                     */
+    int32_t seed;        /* round t uses seed + t (CoCoA.scala:45)            */
+    int32_t chkpt_iter;  /* accepted; RDD lineage truncation has no analogue  */
+    int32_t _pad;
+} cocoa_debug;
+
+/* Evaluation record (OptUtils.scala:57-98).  Rank-local partial sums are
+ * exposed so a multi-GPU caller can all-reduce them. */
+typedef struct {
+    double primal;        /* computePrimalObjective   OptUtils.scala:73     */
+    double dual;          /* computeDualObjective     OptUtils.scala:80     */
+    double gap;           /* computeDualityGap        OptUtils.scala:89     */
+    double test_error;    /* computeClassificationError OptUtils.scala:95   */
+    double hinge_sum;     /* sum_i max(1 - y_i x_i.w, 0) over this rank's train rows */
+    double alpha_sum;     /* sum of this rank's alpha                       */
+    double w_sqnorm;      /* sum_j w_j^2 (raw; norm(w) = sqrt of it)          */
+    int64_t test_err_count; /* misclassified test rows on this rank         */
+    int64_t test_rows;    /* test rows on this rank                         */
+} cocoa_eval_result;
+
+typedef struct cocoa_ctx cocoa_ctx;
+
+/* ---- context ------------------------------------------------------------ */
+/* device: HIP device ordinal.  strict: 1 = bit-exact mode (sequential dots in
+ * stored order, no FMA contraction, exact divisions: bitwise equal to the CPU
+ * restatement), 0 = fast mode (wave-tree dots, FMA; agrees within 1e-9).
+ * stream: a hipStream_t to run on (NULL = a stream owned by the context). */
+int cocoa_create(int device, int strict, void *stream, cocoa_ctx **out);
+int cocoa_destroy(cocoa_ctx *ctx);
+const char *cocoa_last_error(const cocoa_ctx *ctx);
+int cocoa_version(void);
+
+/* ---- data (OptUtils.loadLIBSVMData result, OptUtils.scala:11-53) -------- */
+/* This rank's partitions of the training set as one CSR: rows are
+ * partition-contiguous, partition k owns rows [part_ptr[k], part_ptr[k+1]).
+ * part_begin / num_parts_global: global index of this rank's first partition
+ * and the global K (data.partitions.size, CoCoA.scala:28).  Rows keep their
+ * stored entry order (dot products are summed in that order). */
+int cocoa_set_train(cocoa_ctx *ctx, int32_t num_parts, const int64_t *part_ptr, const int64_t *row_ptr,
+                    const int32_t *col, const double *val, const double *y, int64_t n_rows, int32_t num_features,
+                    int32_t part_begin, int32_t num_parts_global);
+/* This rank's share of DebugParams.testData (any row split). */
+int cocoa_set_test(cocoa_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *val, const double *y,
+                   int64_t n_rows);
+
+/* ---- solver ---------------------------------------------------------------*/
+/* Start a run: alpha = 0 (CoCoA.scala:33), w = w_init (NULL = zeros,
+ * hingeDriver.scala:75), scaling per method (CoCoA.scala:37). */
+int cocoa_init(cocoa_ctx *ctx, const cocoa_params *params, const cocoa_debug *debug, int method, const double *w_init);
+/* Round t (1-based), local half: sampling with seed+t, K local solvers
+ * (CoCoA.localSDCA, CoCoA.scala:130-192 / MinibatchCD.scala:200-240 /
+ * SGD.scala:336-388), alpha update (CoCoA.scala:101) and this rank's ordered
+ * deltaW fold into the device buffer returned by cocoa_dw_sum_device_ptr. */
+int cocoa_round_local(cocoa_ctx *ctx, int32_t t);
+/* Device pointer (double[num_features]) holding this rank's deltaW sum after
+ * cocoa_round_local; a multi-GPU caller all-reduces it in place. */
+int cocoa_dw_sum_device_ptr(cocoa_ctx *ctx, void **out);
+/* Redirect the deltaW sum into caller-owned device memory (e.g. a tensor
+ * that torch.distributed all-reduces).  NULL restores the internal buffer. */
+int cocoa_set_dw_sum_buffer(cocoa_ctx *ctx, void *device_ptr);
+/* w += sum * scaling (CoCoA.scala:47-48; MinibatchCD.scala:157-158;
+ * SGD.scala:303-308). */
+int cocoa_round_apply(cocoa_ctx *ctx);
+/* One full round on a single rank = local + apply. */
+int cocoa_round(cocoa_ctx *ctx, int32_t t);
+/* Objectives over this rank's data (OptUtils.scala:57-98).  With one rank the
+ * fields are the reference's values; with several, all-reduce hinge_sum,
+ * alpha_sum and test_err_count and finish with cocoa_eval_finish. */
+int cocoa_eval(cocoa_ctx *ctx, cocoa_eval_result *out);
+int cocoa_eval_finish(const cocoa_ctx *ctx, double hinge_sum, double alpha_sum, double w_sqnorm,
+                      int64_t test_err_count, int64_t test_rows, cocoa_eval_result *out);
+
+/* Per-round observer for cocoa_run (the reference prints at debugIter). */
+typedef void (*cocoa_round_cb)(void *user, int32_t t, const cocoa_eval_result *ev);
+/* CoCoA.runCoCoA / MinibatchCD.runMbCD / SGD.runSGD on one rank:
+ * init + T rounds (+ eval every debug_iter rounds, reported through cb). */
+int cocoa_run(cocoa_ctx *ctx, const cocoa_params *params, const cocoa_debug *debug, int method,
+              const double *w_init, cocoa_round_cb cb, void *user);
+
+int cocoa_get_w(cocoa_ctx *ctx, double *w_out);           /* num_features */
+int cocoa_get_alpha(cocoa_ctx *ctx, double *alpha_out);   /* this rank's n_rows */
+int cocoa_set_w(cocoa_ctx *ctx, const double *w_in);
+int cocoa_set_alpha(cocoa_ctx *ctx, const double *alpha_in);
+
+/* CoCoA.localSDCA (CoCoA.scala:130-192) for ONE partition of the loaded
+ * training set, as a unit: w (in/out, mutated when plus == 0, like the
+ * reference's alias), alpha (in/out), delta_w (out, num_features),
+ * delta_alpha (out, rows of the partition; may be NULL). */
+int cocoa_local_sdca(cocoa_ctx *ctx, int32_t part, double *w, int32_t local_iters, double lambda, int32_t n,
+                     double *alpha, int32_t seed, int plus, double sigma, double *delta_w, double *delta_alpha);
+
+/* The coordinate sample sequence partition `part` draws in round t
+ * (java.util.Random(seed + t).nextInt(n_k), CoCoA.scala:144,151), computed on
+ * the device; for parity tests. */
+int cocoa_samples(cocoa_ctx *ctx, int32_t part, int32_t seed_plus_t, int32_t count, int32_t *out);
+
+/* ---- profiling --------------------------------------------------------- */
+/* Kernel ids for cocoa_kernel_stats. */
+#define COCOA_K_SAMPLE 0
+#define COCOA_K_SOLVER 1
+#define COCOA_K_FOLD 2
+#define COCOA_K_APPLY 3
+#define COCOA_K_EVAL 4
+#define COCOA_K_COUNT 5
+/* enable = 1: bracket every launch with HIP events on the context stream. */
+int cocoa_stats_enable(cocoa_ctx *ctx, int enable);
+/* total device milliseconds and launch count per kernel id since last reset */
+int cocoa_kernel_stats(cocoa_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
+int cocoa_stats_reset(cocoa_ctx *ctx);
+/* Human-readable description of how the solver was planned (LDS placement). */
+int cocoa_plan_info(cocoa_ctx *ctx, char *buf, int len);
+int cocoa_sync(cocoa_ctx *ctx);
+
+/* ---- host-side data layer (no device needed) ---------------------------- */
+/* A dataset allocated by the library; free with cocoa_dataset_free. */
+typedef struct {
+    int64_t n_rows;
+    int32_t num_features;
+    int32_t num_parts;
+    int64_t nnz;
+    int64_t *row_ptr;   /* n_rows + 1 */
+    int32_t *col;       /* nnz, 0-based */
+    double *val;        /* nnz */
+    double *y;          /* n_rows */
+    int64_t *part_ptr;  /* num_parts + 1 */
+} cocoa_dataset;
+
+/* OptUtils.loadLIBSVMData (OptUtils.scala:11-53): Hadoop-1.0.4 byte splits of
+ * the file into num_splits partitions, label +1 iff the token contains '+'
+ * or parses to 1, 1-based indices -> 0-based. */
+int cocoa_load_libsvm(const char *path, int32_t num_splits, int32_t num_features, cocoa_dataset *out);
+/* Seeded synthetic shapes: kind 0 = rcv1-like sparse
+ * (Zipf columns, tf-idf-like values, unit rows), 1 = epsilon-like dense,
+ * 2 = url-like very sparse binary-ish.  The rows are rows [first_row,
+ * first_row + n_rows) of one seeded stream (first_row a multiple of 4096), so
+ * ranks can generate disjoint shards of one problem (same planted separator).
+ * Partitions are contiguous balanced row blocks.  threads <= 0: all cores. */
+int cocoa_gen_synthetic(int32_t kind, int64_t n_rows, int32_t num_features, double mean_nnz, int32_t num_parts,
+                        uint64_t seed, int64_t first_row, int32_t threads, cocoa_dataset *out);
+void cocoa_dataset_free(cocoa_dataset *ds);
+/* java.util.Random(seed).nextInt(bound) x count on the host (bound <= 0:
+ * nextInt()). */
+int cocoa_jrandom_ints(int64_t seed, int32_t bound, int32_t count, int32_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COCOA_CAPI_H */

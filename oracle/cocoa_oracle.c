@@ -527,7 +527,11 @@ typedef struct {
     double scaling;
     int32_t t_cur;
     double sgd_step;
+    int32_t Kg;        /* global number of partitions (== D.K unless sharded) */
+    double mult;       /* multiplier of the last local round's deltaW sum */
 } oracle_run;
+
+void oracle_run_set_scaling(oracle_run *R);
 
 oracle_run *oracle_run_create(const oracle_data *train, int method, int32_t n, int32_t H, double lambda,
                               double beta, double gamma, int32_t seed, int nthreads) {
@@ -537,12 +541,24 @@ oracle_run *oracle_run_create(const oracle_data *train, int method, int32_t n, i
     R->method = method;
     R->n = n; R->H = H; R->lambda = lambda; R->beta = beta; R->gamma = gamma; R->seed = seed;
     R->nthreads = nthreads < 1 ? 1 : nthreads;
+    R->Kg = train->K;
     int64_t d = train->d, K = train->K;
     R->w = (double *)calloc((size_t)d, sizeof(double));               /* wInit = zeros */
     R->alpha = (double *)calloc((size_t)train->n + 1, sizeof(double));
     R->alpha_old = (double *)calloc((size_t)train->n + 1, sizeof(double));
     R->dw = (double *)calloc((size_t)(K * d), sizeof(double));
     R->wloc = (double *)calloc((size_t)(K * d), sizeof(double));
+    oracle_run_set_scaling(R);
+    return R;
+}
+
+/* scaling per method from the GLOBAL partition count (CoCoA.scala:37,
+ * MinibatchCD.scala:147, SGD.scala:283-288) */
+void oracle_run_set_scaling(oracle_run *R) {
+    const int64_t K = R->Kg;
+    const int32_t H = R->H;
+    const double beta = R->beta, gamma = R->gamma;
+    const int method = R->method;
     /* parts * localIters is Scala Int arithmetic (wraps) */
     const double kh = (double)(int32_t)((uint32_t)K * (uint32_t)H);
     switch (method) {
@@ -552,7 +568,11 @@ oracle_run *oracle_run_create(const oracle_data *train, int method, int32_t n, i
         case M_LOCALSGD: R->scaling = beta / (double)K; break;        /* SGD.scala:285 */
         case M_MBSGD: R->scaling = beta / kh; break;                  /* SGD.scala:287 */
     }
-    return R;
+}
+
+void oracle_run_set_global_parts(oracle_run *R, int32_t Kg) {
+    R->Kg = Kg;
+    oracle_run_set_scaling(R);
 }
 
 void oracle_run_destroy(oracle_run *R) {
@@ -591,7 +611,7 @@ static void partition_update(oracle_run *R, int32_t k, int32_t t, double t0) {
             const double *wsrc = R->w;
             if (!plus) { memcpy(wl, R->w, sizeof(double) * (size_t)d); wsrc = wl; } /* task's private copy */
             oracle_local_sdca(rp, D->col, D->val, D->y + r0, nl, (int32_t)d, (double *)wsrc, R->H, R->lambda, R->n,
-                              al, ao, seed, plus, (double)D->K * R->gamma, dw, NULL);
+                              al, ao, seed, plus, (double)R->Kg * R->gamma, dw, NULL);
         }
         for (int32_t i = 0; i < nl; ++i) al[i] = ao[i] + ((al[i] - ao[i]) * R->scaling); /* CoCoA.scala:101 */
     } else {
@@ -607,8 +627,8 @@ static void *worker(void *p) {
     return NULL;
 }
 
-/* One outer round t (1-based). */
-void oracle_run_round(oracle_run *R, int32_t t) {
+/* One outer round t (1-based), local half: partition updates + ordered fold. */
+void oracle_run_local(oracle_run *R, int32_t t, double *dw_sum) {
     const oracle_data *D = &R->D;
     int64_t d = D->d;
     double t0 = 0.0;
@@ -620,7 +640,7 @@ void oracle_run_round(oracle_run *R, int32_t t) {
             for (int64_t j = 0; j < d; ++j) R->w[j] *= scale;
         }
         /* ((t-1) * localIters * parts) in Scala Int arithmetic (:302) */
-        int32_t ti = (int32_t)((uint32_t)(t - 1) * (uint32_t)R->H * (uint32_t)D->K);
+        int32_t ti = (int32_t)((uint32_t)(t - 1) * (uint32_t)R->H * (uint32_t)R->Kg);
         t0 = (double)ti;
     }
     int nt = R->nthreads < D->K ? R->nthreads : D->K;
@@ -639,9 +659,9 @@ void oracle_run_round(oracle_run *R, int32_t t) {
         for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
         R->nthreads = saved;
     }
-    /* reduce(_ + _) in partition order, then w += sum * scaling (CoCoA.scala:47-48) */
-    double mult = R->scaling;
-    if (R->method == M_MBSGD) mult = R->sgd_step * R->scaling;       /* SGD.scala:307 */
+    /* reduce(_ + _) in partition order (CoCoA.scala:47) */
+    R->mult = R->scaling;
+    if (R->method == M_MBSGD) R->mult = R->sgd_step * R->scaling;    /* SGD.scala:307 */
     for (int64_t j = 0; j < d; ++j) {
         double s = 0.0;
         int have = 0;
@@ -651,9 +671,21 @@ void oracle_run_round(oracle_run *R, int32_t t) {
             s = have ? s + v : v;
             have = 1;
         }
-        R->w[j] += (s * mult);
+        dw_sum[j] = s;
     }
     R->t_cur = t;
+}
+
+/* w += sum * scaling (CoCoA.scala:48) */
+void oracle_run_apply(oracle_run *R, const double *dw_sum) {
+    for (int64_t j = 0; j < R->D.d; ++j) R->w[j] += (dw_sum[j] * R->mult);
+}
+
+void oracle_run_round(oracle_run *R, int32_t t) {
+    double *s = (double *)malloc(sizeof(double) * (size_t)R->D.d);
+    oracle_run_local(R, t, s);
+    oracle_run_apply(R, s);
+    free(s);
 }
 
 /* out: [primal, dual, gap, test_err_count, train_hinge_sum, alpha_sum] */

@@ -52,6 +52,9 @@ def lib():
                                         ctypes.c_int]
         L.oracle_run_destroy.argtypes = [ctypes.c_void_p]
         L.oracle_run_round.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.oracle_run_local.argtypes = [ctypes.c_void_p, ctypes.c_int32, _f64p]
+        L.oracle_run_apply.argtypes = [ctypes.c_void_p, _f64p]
+        L.oracle_run_set_global_parts.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         L.oracle_run_eval.argtypes = [ctypes.c_void_p, ctypes.POINTER(OracleData), _f64p]
         for f in ("oracle_run_get_w", "oracle_run_get_alpha", "oracle_run_set_w", "oracle_run_set_alpha"):
             getattr(L, f).argtypes = [ctypes.c_void_p, _f64p]
@@ -151,6 +154,15 @@ class Run:
 
     def round(self, t):
         lib().oracle_run_round(self.h, t)
+
+    def set_global_parts(self, Kg):
+        lib().oracle_run_set_global_parts(self.h, Kg)
+
+    def round_local(self, t, out):
+        lib().oracle_run_local(self.h, t, _p(out, _f64p))
+
+    def round_apply(self, dw_sum):
+        lib().oracle_run_apply(self.h, _p(np.ascontiguousarray(dw_sum, np.float64), _f64p))
 
     def eval(self, test=None):
         out = np.zeros(6, np.float64)

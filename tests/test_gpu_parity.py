@@ -1,0 +1,289 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+golden fixtures.  Strict mode must be bitwise identical; fast mode must agree
+within the north_star tolerance of 1e-9 relative (error counts exact)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cocoa_amd
+from cocoa_amd import Engine
+from cocoa_amd.data import LabeledData
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+TRAIN = os.path.join(G, "data", "small_train.dat")
+TEST = os.path.join(G, "data", "small_test.dat")
+REL = 1e-9  # BASELINE.json north_star tolerance (fp64, relative)
+
+
+def _j(name):
+    return json.load(open(os.path.join(G, name)))
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, "<f8").tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def c1():
+    return cocoa_amd.load_libsvm(TRAIN, 4, 9947), cocoa_amd.load_libsvm(TEST, 4, 9947)
+
+
+def odata(d):
+    return oracle.Data(d.row_ptr, d.col, d.val, d.y, d.part_ptr, d.num_features)
+
+
+def engine(tr, te=None, strict=True):
+    e = Engine(strict=strict)
+    e.set_train(tr)
+    if te is not None:
+        e.set_test(te)
+    return e
+
+
+# ---------------------------------------------------------------- sampler --
+@pytest.mark.parametrize("seed", [1, 2, 7, 100, -3, 2**31 - 1])
+def test_device_sampler_matches_java_random(c1, seed):
+    tr, _ = c1
+    e = engine(tr)
+    for k in range(4):
+        nl = int(tr.part_ptr[k + 1] - tr.part_ptr[k])
+        got = e.samples(k, seed, 5000)
+        assert np.array_equal(got, oracle.samples(seed, nl, 5000)), (k, seed)
+
+
+def test_device_sampler_power_of_two_and_odd_bounds():
+    # partitions of 512, 1, 3, 1000 rows: power-of-two fast path and rejection loop
+    sizes = [512, 1, 3, 1000]
+    n = sum(sizes)
+    d = cocoa_amd.gen_synthetic("rcv1", n, 500, 10.0, 1, 5)
+    d.part_ptr = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    e = engine(d)
+    for k, nl in enumerate(sizes):
+        for seed in (0, 9, 12345):
+            assert np.array_equal(e.samples(k, seed, 3000), oracle.samples(seed, nl, 3000))
+
+
+# ------------------------------------------------------ unit: localSDCA --
+@pytest.mark.parametrize("plus", [True, False])
+def test_local_sdca_unit_strict_matches_golden(c1, plus):
+    tr, _ = c1
+    fx = _j("c1_localsdca_%s.json" % ("plus" if plus else "cocoa"))
+    w = np.zeros(9947)
+    w[::7] = ((np.arange(0, 9947, 7) % 13) - 6) * 1e-3
+    part = fx["part"]
+    nl = int(tr.part_ptr[part + 1] - tr.part_ptr[part])
+    a = np.zeros(nl)
+    a[::3] = 0.5
+    e = engine(tr, strict=True)
+    da, dw = e.local_sdca(part, w, fx["H"], fx["lam"], fx["n"], a, fx["seed"], plus, fx["sigma"])
+    assert sha(dw) == fx["dw_sha256"]
+    assert sha(a) == fx["alpha_sha256"]
+    assert sha(w) == fx["w_out_sha256"]
+
+
+@pytest.mark.parametrize("plus", [True, False])
+def test_local_sdca_unit_fast_within_tolerance(c1, plus):
+    tr, _ = c1
+    od = odata(tr)
+    w = np.linspace(-0.01, 0.01, 9947)
+    a0 = np.zeros(int(tr.part_ptr[3] - tr.part_ptr[2]))
+    a0[::5] = 0.3
+    wr, ar = w.copy(), a0.copy()
+    _, dwr = oracle.local_sdca(od, 2, wr, 400, 1e-3, 2000, ar, 11, plus, 4.0)
+    wg, ag = w.copy(), a0.copy()
+    _, dwg = engine(tr, strict=False).local_sdca(2, wg, 400, 1e-3, 2000, ag, 11, plus, 4.0)
+    assert np.max(np.abs(dwg - dwr)) <= REL * np.max(np.abs(dwr))
+    assert np.max(np.abs(ag - ar)) <= REL
+    assert np.max(np.abs(wg - wr)) <= REL * np.max(np.abs(wr))
+
+
+# --------------------------------------------------- full runs: config C1 --
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"])
+def test_c1_strict_run_bitwise_golden(c1, method):
+    tr, te = c1
+    fx = _j("c1_%s.json" % method.replace("+", "plus"))
+    cfg = _j("c1_meta.json")["config"]
+    e = engine(tr, te, strict=True)
+    e.init(method, tr.n, cfg["T"], cfg["H"], cfg["lam"], cfg["beta"], cfg["gamma"], cfg["debug_iter"], cfg["seed"])
+    recs = {r["t"]: r for r in fx["trace"]}
+    for t in range(1, cfg["T"] + 1):
+        e.round(t)
+        if t in recs:
+            ev = e.eval()
+            assert ev["primal"].hex() == recs[t]["primal"], t
+            if "dual" in recs[t]:
+                assert ev["dual"].hex() == recs[t]["dual"], t
+                assert ev["gap"].hex() == recs[t]["gap"], t
+            assert ev["test_err_count"] == recs[t]["test_err"], t
+    assert sha(e.w()) == fx["w_sha256"]
+    if method in ("cocoa+", "cocoa", "mbcd"):
+        assert sha(e.alpha()) == fx["alpha_sha256"]
+
+
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd"])
+def test_c1_fast_run_within_tolerance(c1, method):
+    tr, te = c1
+    fx = _j("c1_%s.json" % method.replace("+", "plus"))
+    cfg = _j("c1_meta.json")["config"]
+    e = engine(tr, te, strict=False)
+    e.init(method, tr.n, cfg["T"], cfg["H"], cfg["lam"], cfg["beta"], cfg["gamma"], cfg["debug_iter"], cfg["seed"])
+    recs = {r["t"]: r for r in fx["trace"]}
+    for t in range(1, cfg["T"] + 1):
+        e.round(t)
+        if t in recs:
+            ev = e.eval()
+            P, D = float.fromhex(recs[t]["primal"]), float.fromhex(recs[t]["dual"])
+            assert abs(ev["primal"] - P) <= REL * abs(P)
+            assert abs(ev["dual"] - D) <= REL * abs(D)
+            assert abs(ev["gap"] - (P - D)) <= REL * abs(P)
+            assert ev["test_err_count"] == recs[t]["test_err"]
+
+
+def test_c1_run_api_and_callback(c1):
+    tr, te = c1
+    seen = []
+    e = engine(tr, te, strict=True)
+    e.run("cocoa+", tr.n, 30, 50, 1e-3, debug_iter=10, callback=lambda t, ev: seen.append((t, ev["primal"])))
+    fx = _j("c1_cocoaplus.json")
+    assert [t for t, _ in seen] == [10, 20, 30]
+    assert [p.hex() for _, p in seen] == [r["primal"] for r in fx["trace"][:3]]
+
+
+# ------------------------------------------------------------- edge cases --
+def _dataset_with_edges(seed=3):
+    rng = np.random.default_rng(seed)
+    d = 3000
+    rows = []
+    for r in range(900):
+        if r % 97 == 5:
+            z = 0                                   # empty row
+        elif r % 131 == 7:
+            z = 2500                                # longer than the LDS stream buffer
+        elif r % 53 == 3:
+            z = 300                                 # beyond the register fast path
+        else:
+            z = int(rng.integers(1, 80))
+        cols = np.sort(rng.choice(d, size=z, replace=False)).astype(np.int32)
+        if r % 71 == 9 and z > 3:
+            cols[2] = cols[1]                       # duplicate column index in a row
+        vals = rng.standard_normal(z)
+        vals /= max(np.linalg.norm(vals), 1e-300)
+        rows.append((cols, vals))
+    row_ptr = np.concatenate([[0], np.cumsum([len(c) for c, _ in rows])]).astype(np.int64)
+    y = np.where(rng.random(900) < 0.5, 1.0, -1.0)
+    part = np.array([0, 250, 251, 600, 900], np.int64)   # includes a 1-row partition
+    return LabeledData(row_ptr, np.concatenate([c for c, _ in rows]).astype(np.int32),
+                       np.concatenate([v for _, v in rows]), y, part, d)
+
+
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"])
+@pytest.mark.parametrize("gamma,beta", [(1.0, 1.0), (0.25, 2.0)])
+def test_edge_rows_strict_bitwise_vs_oracle(method, gamma, beta):
+    tr = _dataset_with_edges()
+    te = tr.row_range(0, 400)
+    od, ot = odata(tr), odata(te)
+    H = 120
+    run = oracle.Run(od, method, tr.n, H, 2e-3, beta, gamma, seed=5)
+    e = engine(tr, te, strict=True)
+    e.init(method, tr.n, 6, H, 2e-3, beta, gamma, 1, 5)
+    for t in range(1, 7):
+        run.round(t)
+        e.round(t)
+        ev, rv = e.eval(), run.eval(ot)
+        assert ev["primal"].hex() == rv["primal"].hex(), t
+        if method in ("cocoa+", "cocoa", "mbcd"):
+            assert ev["gap"].hex() == rv["gap"].hex(), t
+        assert ev["test_err_count"] == rv["test_err"]
+    assert np.array_equal(e.w(), run.w())
+    assert np.array_equal(e.alpha(), run.alpha())
+
+
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd"])
+def test_edge_rows_fast_within_tolerance(method):
+    tr = _dataset_with_edges(4)
+    od = odata(tr)
+    run = oracle.Run(od, method, tr.n, 150, 2e-3, seed=1)
+    e = engine(tr, strict=False)
+    e.init(method, tr.n, 5, 150, 2e-3, 1.0, 1.0, 1, 1)
+    for t in range(1, 6):
+        run.round(t)
+        e.round(t)
+    wr = run.w()
+    assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+    assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
+
+
+def test_empty_partition_is_an_error():
+    tr = _dataset_with_edges()
+    tr.part_ptr = np.array([0, 250, 250, 900], np.int64)
+    e = engine(tr)
+    with pytest.raises(cocoa_amd.IllegalArgumentError):
+        e.init("cocoa+", tr.n, 1, 10, 1e-3)
+
+
+def test_fast_eval_matches_oracle_on_same_state(c1):
+    tr, te = c1
+    od, ot = odata(tr), odata(te)
+    run = oracle.Run(od, "cocoa+", tr.n, 50, 1e-3)
+    for t in range(1, 21):
+        run.round(t)
+    e = engine(tr, te, strict=False)
+    e.init("cocoa+", tr.n, 0, 50, 1e-3)
+    e.set_w(run.w())
+    e.set_alpha(run.alpha())
+    ev, rv = e.eval(), run.eval(ot)
+    for k in ("primal", "dual"):
+        assert abs(ev[k] - rv[k]) <= 1e-13 * abs(rv[k])
+    assert ev["test_err_count"] == rv["test_err"]
+
+
+# ------------------------------------------------ full BASELINE-size shape --
+@pytest.fixture(scope="module")
+def c2():
+    # config C2: rcv1-shaped, n=677,399, d=47,236, K=64
+    return cocoa_amd.gen_synthetic("rcv1", 677399, 47236, 75.6, 64, 12345)
+
+
+def test_c2_strict_round_bitwise_vs_oracle(c2):
+    H = 677399 // 64
+    od = odata(c2)
+    run = oracle.Run(od, "cocoa+", c2.n, H, 1e-4, nthreads=16)
+    e = engine(c2, strict=True)
+    e.init("cocoa+", c2.n, 2, H, 1e-4, debug_iter=1)
+    for t in (1, 2):
+        run.round(t)
+        e.round(t)
+    assert np.array_equal(e.w(), run.w())
+    assert np.array_equal(e.alpha(), run.alpha())
+    ev = e.eval()
+    assert ev["primal"].hex() == od.primal(run.w(), 1e-4).hex()
+
+
+def test_c2_fast_properties(c2):
+    """Size-independent properties at full size: fast agrees with strict within
+    1e-9, weak duality holds, alpha stays in the box, the gap shrinks."""
+    H = 677399 // 64
+    f = engine(c2, strict=False)
+    s = engine(c2, strict=True)
+    f.init("cocoa+", c2.n, 4, H, 1e-4)
+    s.init("cocoa+", c2.n, 4, H, 1e-4)
+    gaps = []
+    for t in range(1, 5):
+        f.round(t)
+        s.round(t)
+        ev = f.eval()
+        assert ev["gap"] >= 0.0
+        gaps.append(ev["gap"])
+    ws, wf = s.w(), f.w()
+    assert np.max(np.abs(wf - ws)) <= REL * np.max(np.abs(ws))
+    a = f.alpha()
+    assert a.min() >= 0.0 and a.max() <= 1.0
+    assert gaps[-1] < gaps[0]
+    es = s.eval()
+    assert abs(es["primal"] - f.eval()["primal"]) <= REL * es["primal"]
