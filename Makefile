@@ -27,6 +27,16 @@ $(OUT): $(OBJS)
 cocoa_amd/cocoa_driver: $(CSRC)/driver_main.cpp $(OUT) include/cocoa_capi.h
 	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude -x c++ $< -o $@ -Lcocoa_amd -lcocoa_hip -Wl,-rpath,'$$ORIGIN'
 
+# diagnostic build with per-step phase stamps in the local solver
+DIAG := build/diag
+diag: $(DIAG)/libcocoa_hip.so
+$(DIAG)/libcocoa_hip.so: $(CSRC)/*.hip $(CSRC)/*.cpp $(HDRS)
+	mkdir -p $(DIAG)
+	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -ffp-contract=off -c $(CSRC)/kernels_strict.hip -o $(DIAG)/ks.o
+	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -ffp-contract=fast -munsafe-fp-atomics -c $(CSRC)/kernels_fast.hip -o $(DIAG)/kf.o
+	$(HIPCC) $(COMMON) -ffp-contract=off -c $(CSRC)/engine.hip -o $(DIAG)/en.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DIAG)/ks.o $(DIAG)/kf.o $(DIAG)/en.o $(BUILD)/dataset.o -lpthread
+
 oracle/liboracle.so: oracle/cocoa_oracle.c
 	$(MAKE) -s -C oracle
 
@@ -36,4 +46,4 @@ $(BUILD):
 clean:
 	rm -rf build $(OUT) cocoa_amd/cocoa_driver oracle/liboracle.so
 
-.PHONY: all clean
+.PHONY: all clean diag

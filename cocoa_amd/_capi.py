@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcocoa_hip.so")
+# COCOA_LIB may point at a diagnostic build (e.g. build/diag/libcocoa_hip.so)
+LIB_PATH = os.environ.get("COCOA_LIB") or os.path.join(HERE, "libcocoa_hip.so")
 
 COCOA_OK = 0
 E_ARG, E_PARSE, E_RANGE, E_IO, E_HIP, E_STATE, E_NODEV = -1, -2, -3, -4, -5, -6, -7
@@ -107,6 +108,8 @@ SIGNATURES = {
     "cocoa_kernel_stats": (_int, [_vp, _int, _pf64, _pi64]),
     "cocoa_stats_reset": (_int, [_vp]),
     "cocoa_plan_info": (_int, [_vp, ctypes.c_char_p, _int]),
+    "cocoa_solver_profile": (_int, [_vp, _int]),
+    "cocoa_solver_profile_read": (_int, [_vp, ctypes.POINTER(ctypes.c_uint64), _i64]),
     "cocoa_sync": (_int, [_vp]),
     "cocoa_load_libsvm": (_int, [ctypes.c_char_p, _i32, _i32, ctypes.POINTER(Dataset)]),
     "cocoa_gen_synthetic": (_int, [_i32, _i64, _i32, _f64, _i32, ctypes.c_uint64, _i64, _i32,

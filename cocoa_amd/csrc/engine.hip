@@ -104,7 +104,7 @@ struct cocoa_ctx {
     cocoa_params P{};
     cocoa_debug D{};
     double scaling = 1.0, mult = 1.0;
-    DevBuf w, alpha, alpha_work, dw, wloc, samples, dw_sum_int, eval_part, eval_out, row_scratch, jump;
+    DevBuf w, alpha, alpha_work, dw, wloc, samples, dw_sum_int, eval_part, eval_out, row_scratch, jump, prof;
     double* dw_sum = nullptr;
     double* h_eval = nullptr;  // pinned [4]
     int64_t samples_cap = 0;
@@ -469,6 +469,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.H = H;
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 0;
+    a.prof = nullptr;
     a.lam_n = params->lambda * (double)params->n;
     a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
     a.scaling = ctx->scaling;
@@ -721,6 +722,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     a.H = local_iters;
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 1;
+    a.prof = nullptr;
     a.lam_n = lambda * (double)n;
     a.sigma = sigma;
     a.scaling = 1.0;
@@ -783,6 +785,27 @@ extern "C" int cocoa_stats_reset(cocoa_ctx* ctx) {
     CAPI_BEGIN(ctx)
     ctx->drain();
     for (int i = 0; i < COCOA_K_COUNT; ++i) ctx->tot_ms[i] = 0, ctx->cnt[i] = 0;
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    if (enable) {
+        ctx->prof.alloc_zero(sizeof(uint64_t) * (size_t)ctx->K_loc * 32, ctx->stream);
+        ctx->sa.prof = ctx->prof.as<uint64_t>();
+    } else {
+        ctx->sa.prof = nullptr;
+    }
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_solver_profile_read(cocoa_ctx* ctx, uint64_t* out, int64_t count) {
+    CAPI_BEGIN(ctx)
+    require(out && ctx->prof.p, COCOA_E_STATE, "solver profiling not enabled");
+    const size_t n = std::min<size_t>((size_t)count, (size_t)ctx->K_loc * 32);
+    HIPCHK(hipMemcpyAsync(out, ctx->prof.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
     CAPI_END(ctx)
 }
 

@@ -60,6 +60,7 @@ struct SolverArgs {
     int32_t lds_scratch;      // compute scratch: kRegChunks*64 doubles
     int32_t lds_vec;          // d doubles (deltaW, or w_loc for CoCoA) if VEC_LDS
     int32_t lds_alpha;        // rows-of-largest-partition doubles if ALPHA_LDS
+    uint64_t* prof;           // optional cycle counters [K][2 waves][16] (diagnostics)
 };
 
 struct EvalArgs {

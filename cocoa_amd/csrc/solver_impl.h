@@ -154,13 +154,35 @@ __device__ __forceinline__ double dot_regs(const double (&prod)[kRegChunks], int
     }
 }
 
+#ifdef COCOA_STEP_PROF
+// diagnostic build only: per-step phase stamps (shares, not absolute times)
+#define STEP_STAMP(i)                \
+    do {                             \
+        const uint64_t c_ = clock64(); \
+        sp[i] += c_ - last_;         \
+        last_ = c_;                  \
+    } while (0)
+#define STEP_KEEP(x) asm volatile("" ::"v"(x))
+#else
+#define STEP_STAMP(i) \
+    do {              \
+    } while (0)
+#define STEP_KEEP(x) \
+    do {             \
+    } while (0)
+#endif
+
 template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS>
 __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const int32_t* scol, const double* sval,
-                              double* scratch, double* vec, double* dwk, double* alv) {
+                              double* scratch, double* vec, double* dwk, double* alv, uint64_t (&sp)[6]) {
     const int lane = lane_id();
     const int m = uni(mb->m);
     const double lam_n = a.lam_n;
     const double sigma = a.sigma;
+#ifdef COCOA_STEP_PROF
+    uint64_t last_ = clock64();
+#endif
+    (void)sp;
     for (int s = 0; s < m; ++s) {
         const int32_t r = uni(mb->r[s]);
         const int32_t off = uni(mb->off[s]);
@@ -170,6 +192,7 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
         const double qv = uni(mb->q[s]);
         const double xw = MODE != MODE_COCOA ? uni(mb->xw[s]) : 0.0;
         const double aa = uni(alv[r]);  // after the previous step's write (in order)
+        STEP_STAMP(0);
 
         const bool fast_path = off >= 0 && z <= 64 * kRegChunks && (fl & 1) == 0;
         int32_t pc[kRegChunks];
@@ -189,10 +212,14 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
                 }
             }
             if (MODE != MODE_MBCD) {
+#pragma unroll
+                for (int u = 0; u < kRegChunks; ++u) STEP_KEEP(pd[u]);
+                STEP_STAMP(1);
                 double prod[kRegChunks];
 #pragma unroll
                 for (int u = 0; u < kRegChunks; ++u) prod[u] = pv[u] * pd[u];
                 sdot = dot_regs<STRICT>(prod, z, scratch);
+                STEP_STAMP(2);
             }
         } else if (MODE != MODE_MBCD) {
             // generic path: long / unstaged / duplicate-column rows
@@ -234,6 +261,8 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
             double na = 1.0;
             if (qii != 0.0) na = jmin(jmax((aa - (grad / qii)), 0.0), 1.0);
             const double coef = (yv * (na - aa)) / lam_n;        // CoCoA.scala:181
+            STEP_KEEP(coef);
+            STEP_STAMP(3);
             if (fast_path) {
 #pragma unroll
                 for (int u = 0; u < kRegChunks; ++u) {
@@ -279,6 +308,7 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
             }
             if (lane == 0) alv[r] = na;                          // CoCoA.scala:186
         }
+        STEP_STAMP(4);
     }
 }
 
@@ -313,10 +343,13 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
         load_batch<MODE, STRICT>(a, k, p0, cursor, (BatchMeta*)(lds + a.lds_meta[0]), (int32_t*)(lds + a.lds_stream_col[0]),
                                  (double*)(lds + a.lds_stream_val[0]), prod);
     __syncthreads();
+    uint64_t t_busy = 0, t_wait = 0, n_batch = 0;
+    uint64_t step_prof[6] = {0, 0, 0, 0, 0, 0};
     for (int b = 0;; ++b) {
         const int cur = b & 1;
         const BatchMeta* mb = (const BatchMeta*)(lds + a.lds_meta[cur]);
         if (mb->m == 0) break;
+        const uint64_t c0 = a.prof ? clock64() : 0;
         if (wave == 1) {
             load_batch<MODE, STRICT>(a, k, p0, cursor, (BatchMeta*)(lds + a.lds_meta[cur ^ 1]),
                                      (int32_t*)(lds + a.lds_stream_col[cur ^ 1]), (double*)(lds + a.lds_stream_val[cur ^ 1]),
@@ -324,9 +357,23 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
         } else {
             compute_batch<MODE, STRICT, VEC_LDS, ALPHA_LDS>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
                                                             (const double*)(lds + a.lds_stream_val[cur]), scratch, vec,
-                                                            dwk, alv);
+                                                            dwk, alv, step_prof);
         }
+        const uint64_t c1 = a.prof ? clock64() : 0;
         __syncthreads();
+        if (a.prof) {
+            t_busy += c1 - c0;
+            t_wait += clock64() - c1;
+            n_batch += 1;
+        }
+    }
+    if (a.prof && (tid & 63) == 0) {
+        // [block][wave][busy, wait, batches, step stamps x6]  (16 per wave)
+        uint64_t* pr = a.prof + ((size_t)k * 2 + wave) * 16;
+        pr[0] = t_busy;
+        pr[1] = t_wait;
+        pr[2] = n_batch;
+        for (int i = 0; i < 6; ++i) pr[3 + i] = step_prof[i];
     }
     // epilogue: alpha = alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101,
     // MinibatchCD.scala:242-243)

@@ -138,6 +138,15 @@ class Engine:
             out[name] = {"total_ms": ms.value, "launches": cnt.value}
         return out
 
+    def solver_profile(self, on=True):
+        C.check(C.lib().cocoa_solver_profile(self.h, 1 if on else 0), self.h)
+
+    def solver_profile_read(self):
+        out = np.zeros(self.K_loc * 32, np.uint64)
+        C.check(C.lib().cocoa_solver_profile_read(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                                  len(out)), self.h)
+        return out.reshape(self.K_loc, 2, 16)
+
     def plan(self):
         buf = ctypes.create_string_buffer(1024)
         C.check(C.lib().cocoa_plan_info(self.h, buf, 1024), self.h)

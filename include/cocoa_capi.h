@@ -171,6 +171,12 @@ int cocoa_stats_enable(cocoa_ctx *ctx, int enable);
 /* total device milliseconds and launch count per kernel id since last reset */
 int cocoa_kernel_stats(cocoa_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
 int cocoa_stats_reset(cocoa_ctx *ctx);
+/* Diagnostics: per-workgroup cycle counters of the local-solver kernel
+ * (uint64 [K_loc][2 waves][16]: busy cycles, barrier-wait cycles, batches,
+ * then per-step phase cycles in a -DCOCOA_STEP_PROF build).  Overwritten by
+ * every solver launch while enabled. */
+int cocoa_solver_profile(cocoa_ctx *ctx, int enable);
+int cocoa_solver_profile_read(cocoa_ctx *ctx, uint64_t *out, int64_t count);
 /* Human-readable description of how the solver was planned (LDS placement). */
 int cocoa_plan_info(cocoa_ctx *ctx, char *buf, int len);
 int cocoa_sync(cocoa_ctx *ctx);
