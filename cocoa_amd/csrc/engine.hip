@@ -97,6 +97,22 @@ struct cocoa_ctx {
     // test data (this rank)
     Csr te;
     bool has_test = false;
+    // row tiles of the fast evaluation pass
+    DevBuf tiles, t_tiles;
+    int64_t n_tiles = 0, n_t_tiles = 0;
+    // device feature order (see cocoa_set_train)
+    std::vector<int32_t> perm, inv;
+    std::vector<int64_t> n_hot_nnz;
+    DevBuf d_perm, d_inv;
+
+    // host <-> device order of a w-like vector
+    void to_device_order(const double* orig, std::vector<double>& dev) const {
+        dev.resize((size_t)d);
+        for (int32_t j = 0; j < d; ++j) dev[(size_t)perm[(size_t)j]] = orig[j];
+    }
+    void to_host_order(const std::vector<double>& dev, double* orig) const {
+        for (int32_t j = 0; j < d; ++j) orig[j] = dev[(size_t)perm[(size_t)j]];
+    }
 
     // run state
     bool inited = false;
@@ -264,6 +280,25 @@ static void upload(DevBuf& b, const void* src, size_t bytes, hipStream_t s) {
     if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s));
 }
 
+// Row tiles for the fast eval pass: whole rows, <= kEvalTile entries and rows
+// per tile; a row longer than kEvalTile is a tile of its own.
+static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStream_t s) {
+    std::vector<int64_t> t{0};
+    int64_t r = 0;
+    while (r < n) {
+        const int64_t start = r, e0 = row_ptr[r];
+        if (row_ptr[r + 1] - e0 > kEvalTile) {
+            ++r;
+        } else {
+            while (r < n && row_ptr[r + 1] - e0 <= kEvalTile && r - start < kEvalTile) ++r;
+        }
+        t.push_back(r);
+    }
+    upload(out, t.data(), sizeof(int64_t) * t.size(), s);
+    HIPCHK(hipStreamSynchronize(s));
+    return (int64_t)t.size() - 1;
+}
+
 static void check_csr(const int64_t* row_ptr, const int32_t* col, int64_t n, int32_t d) {
     require(row_ptr[0] == 0, COCOA_E_ARG, "row_ptr[0] must be 0");
     for (int64_t r = 0; r < n; ++r) require(row_ptr[r + 1] >= row_ptr[r], COCOA_E_ARG, "row_ptr not monotone");
@@ -325,14 +360,38 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
             if (fl[(size_t)r]) ctx->any_dup = true;
         }
     }
+    // Device feature order: columns relabelled by descending frequency in this
+    // rank's rows (ties by index) so the hottest coordinates of deltaW are the
+    // first ones (the LDS-resident slice of the solver).  Entry order inside a
+    // row is unchanged, so every dot product sums the same terms in the same
+    // order; w crosses the C ABI in the original order.
+    {
+        std::vector<int64_t> freq((size_t)num_features, 0);
+        for (int64_t q = 0; q < nnz; ++q) freq[(size_t)col[q]]++;
+        std::vector<int32_t> order((size_t)num_features);
+        for (int32_t j = 0; j < num_features; ++j) order[(size_t)j] = j;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int32_t x, int32_t y) { return freq[(size_t)x] > freq[(size_t)y]; });
+        ctx->inv.assign(order.begin(), order.end());            // new -> old
+        ctx->perm.assign((size_t)num_features, 0);              // old -> new
+        for (int32_t j = 0; j < num_features; ++j) ctx->perm[(size_t)order[(size_t)j]] = j;
+        ctx->n_hot_nnz.assign((size_t)num_features + 1, 0);      // nnz share of the first j columns
+        for (int32_t j = 0; j < num_features; ++j)
+            ctx->n_hot_nnz[(size_t)j + 1] = ctx->n_hot_nnz[(size_t)j] + freq[(size_t)order[(size_t)j]];
+    }
+    std::vector<int32_t> pcol((size_t)std::max<int64_t>(nnz, 1));
+    for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];
     hipStream_t s = ctx->stream;
+    upload(ctx->d_perm, ctx->perm.data(), sizeof(int32_t) * (size_t)num_features, s);
+    upload(ctx->d_inv, ctx->inv.data(), sizeof(int32_t) * (size_t)num_features, s);
     upload(ctx->tr.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
-    upload(ctx->tr.col, col, sizeof(int32_t) * (size_t)nnz, s);
+    upload(ctx->tr.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
     upload(ctx->tr.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
+    ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s);
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
     CAPI_END(ctx)
@@ -348,10 +407,13 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
     hipStream_t s = ctx->stream;
     ctx->te.n = n_rows;
     ctx->te.nnz = nnz;
+    std::vector<int32_t> pcol((size_t)std::max<int64_t>(nnz, 1));
+    for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];  // device feature order
     upload(ctx->te.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
-    upload(ctx->te.col, col, sizeof(int32_t) * (size_t)nnz, s);
+    upload(ctx->te.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
     upload(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
+    ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s);
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     if (ctx->inited) {
@@ -429,9 +491,11 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     }
     hipStream_t s = ctx->stream;
     ctx->w.alloc(sizeof(double) * (size_t)d);
-    if (w_init)
-        HIPCHK(hipMemcpyAsync(ctx->w.p, w_init, sizeof(double) * (size_t)d, hipMemcpyHostToDevice, s));
-    else
+    std::vector<double> wdev;
+    if (w_init) {
+        ctx->to_device_order(w_init, wdev);
+        HIPCHK(hipMemcpyAsync(ctx->w.p, wdev.data(), sizeof(double) * (size_t)d, hipMemcpyHostToDevice, s));
+    } else
         HIPCHK(hipMemsetAsync(ctx->w.p, 0, sizeof(double) * (size_t)d, s));
     ctx->alpha.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
     ctx->alpha_work.alloc(sizeof(double) * (size_t)std::max<int64_t>(n, 1));
@@ -514,7 +578,8 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         c->mult = step * c->scaling;
     }
     c->timed(COCOA_K_FOLD, [&] {
-        launch_fold(c->dw.as<double>(), K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, s);
+        launch_fold(c->dw.as<double>(), K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply,
+                    c->d_inv.as<int32_t>(), s);
     });
 }
 
@@ -541,7 +606,9 @@ extern "C" int cocoa_set_dw_sum_buffer(cocoa_ctx* ctx, void* device_ptr) {
 extern "C" int cocoa_round_apply(cocoa_ctx* ctx) {
     CAPI_BEGIN(ctx)
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
-    ctx->timed(COCOA_K_APPLY, [&] { launch_apply(ctx->w.as<double>(), ctx->dw_sum, ctx->d, ctx->mult, ctx->stream); });
+    ctx->timed(COCOA_K_APPLY, [&] {
+        launch_apply(ctx->w.as<double>(), ctx->dw_sum, ctx->d, ctx->mult, ctx->d_inv.as<int32_t>(), ctx->stream);
+    });
     CAPI_END(ctx)
 }
 
@@ -588,15 +655,20 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     e.w = ctx->w.as<double>();
     e.d = ctx->d;
     e.part_ptr = ctx->part_ptr.as<int64_t>();
+    e.perm = ctx->d_perm.as<int32_t>();
     e.K = ctx->K_loc;
     e.partials = ctx->eval_part.as<double>();
     e.out = ctx->eval_out.as<double>();
     e.row_scratch = ctx->row_scratch.as<double>();
+    e.tiles = ctx->tiles.as<int64_t>();
+    e.n_tiles = ctx->n_tiles;
+    e.t_tiles = ctx->has_test ? ctx->t_tiles.as<int64_t>() : nullptr;
+    e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles : 0;
     ctx->timed(COCOA_K_EVAL, [&] {
         if (ctx->strict)
             launch_eval_strict(e, ctx->stream);
         else
-            launch_eval_fast(e, eval_fast_blocks(e.n, e.n_test), ctx->stream);
+            launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
     });
     HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -638,8 +710,10 @@ extern "C" int cocoa_sync(cocoa_ctx* ctx) {
 extern "C" int cocoa_get_w(cocoa_ctx* ctx, double* w_out) {
     CAPI_BEGIN(ctx)
     require(ctx->inited && w_out, COCOA_E_STATE, "cocoa_get_w: not initialised");
-    HIPCHK(hipMemcpyAsync(w_out, ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<double> dev((size_t)ctx->d);
+    HIPCHK(hipMemcpyAsync(dev.data(), ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->to_host_order(dev, w_out);
     CAPI_END(ctx)
 }
 
@@ -656,7 +730,9 @@ extern "C" int cocoa_get_alpha(cocoa_ctx* ctx, double* alpha_out) {
 extern "C" int cocoa_set_w(cocoa_ctx* ctx, const double* w_in) {
     CAPI_BEGIN(ctx)
     require(ctx->inited && w_in, COCOA_E_STATE, "cocoa_set_w: not initialised");
-    HIPCHK(hipMemcpyAsync(ctx->w.p, w_in, sizeof(double) * (size_t)ctx->d, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<double> dev;
+    ctx->to_device_order(w_in, dev);
+    HIPCHK(hipMemcpyAsync(ctx->w.p, dev.data(), sizeof(double) * (size_t)ctx->d, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     CAPI_END(ctx)
 }
@@ -698,7 +774,9 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     upload(pp, h_pp, sizeof(h_pp), s);
     smp.alloc(sizeof(int32_t) * (size_t)std::max(local_iters, 1));
     dwb.alloc_zero(sizeof(double) * (size_t)d, s);
-    upload(wb, w, sizeof(double) * (size_t)d, s);
+    std::vector<double> wdev;
+    ctx->to_device_order(w, wdev);
+    upload(wb, wdev.data(), sizeof(double) * (size_t)d, s);
     if (!plus) wl.alloc(sizeof(double) * (size_t)d);
     al.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(ctx->tr.n, 1), s);
     alw.alloc(sizeof(double) * (size_t)std::max<int64_t>(ctx->tr.n, 1));
@@ -734,13 +812,14 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
             launch_solver_fast(plus ? MODE_PLUS : MODE_COCOA, c.vec_lds, c.alpha_lds, a, 1, c.lds_bytes, s);
         HIPCHK(hipGetLastError());
     }
-    launch_fold(dwb.as<double>(), 1, d, sumb.as<double>(), nullptr, 1.0, false, s);
+    launch_fold(dwb.as<double>(), 1, d, sumb.as<double>(), nullptr, 1.0, false, ctx->d_inv.as<int32_t>(), s);
     HIPCHK(hipGetLastError());
     std::vector<double> old(alpha, alpha + nl);
     HIPCHK(hipMemcpyAsync(delta_w, sumb.p, sizeof(double) * (size_t)d, hipMemcpyDeviceToHost, s));
     if (nl) HIPCHK(hipMemcpyAsync(alpha, al.as<double>() + p0, sizeof(double) * (size_t)nl, hipMemcpyDeviceToHost, s));
-    if (!plus) HIPCHK(hipMemcpyAsync(w, wl.p, sizeof(double) * (size_t)d, hipMemcpyDeviceToHost, s));
+    if (!plus) HIPCHK(hipMemcpyAsync(wdev.data(), wl.p, sizeof(double) * (size_t)d, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (!plus) ctx->to_host_order(wdev, w);
     if (delta_alpha)
         for (int32_t i = 0; i < nl; ++i) delta_alpha[i] = alpha[i] - old[(size_t)i];  // CoCoA.scala:190
     if (ctx->inited) plan_solver(ctx);

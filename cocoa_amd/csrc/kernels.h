@@ -15,6 +15,7 @@ enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2 };
 constexpr int kWave = 64;
 constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
 constexpr int kRegChunks = 4;       // rows with z <= 256 keep (col,val,vec) in registers
+constexpr int kEvalTile = 2048;     // entries (and max rows) per fast-eval tile
 
 // Per-batch step metadata, staged by the loader wave in LDS (SoA).
 struct BatchMeta {
@@ -81,8 +82,15 @@ struct EvalArgs {
     int64_t d;
     // partitions (strict fold order)
     const int64_t* part_ptr;
+    const int32_t* perm;      // original -> device feature order (strict ||w|| order)
     int32_t K;
     int32_t pad;
+    // row tiles for the fast pass: tile t covers rows [tiles[t], tiles[t+1]) whose
+    // entries fit kEvalTile (or one longer row)
+    const int64_t* tiles;
+    int64_t n_tiles;
+    const int64_t* t_tiles;
+    int64_t n_t_tiles;
     // outputs
     double* partials;         // [blocks][4] fast; per-row scratch strict
     double* out;              // [4]: hinge_sum, alpha_sum, w_sq(norm^2 via sqrt), test_err_count
@@ -101,9 +109,11 @@ void launch_solver_strict(int mode, bool vec_lds, bool alpha_lds, const SolverAr
 void launch_eval_strict(const EvalArgs& a, hipStream_t s);
 void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H, int32_t* samples,
                     const uint64_t* jump_tab, hipStream_t s);
+// inv (device order -> original feature index) places the unapplied sum in the
+// original order, the order ranks exchange it in
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
-                 hipStream_t s);
-void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, hipStream_t s);
+                 const int32_t* inv, hipStream_t s);
+void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const int32_t* inv, hipStream_t s);
 void launch_scale(double* w, int64_t d, double scale, hipStream_t s);
 void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, double* out, hipStream_t s);
 void launch_sgd(bool local, const SolverArgs& a, double lambda, double t0, int grid, hipStream_t s);

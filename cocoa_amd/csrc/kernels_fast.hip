@@ -13,60 +13,102 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
 }
 
 // ----------------------------------------------------------- fused eval --
-// One pass over train + test CSR (OptUtils.scala:57-98): 16-lane groups per
-// row (one DPP row), 4 entries per lane in flight, w gathered from L2; the
-// same launch sums alpha and ||w||^2.  Block partials -> fixed-order final
-// reduction (deterministic run to run).
+// One pass over train + test CSR (OptUtils.scala:57-98) as a CSR stream:
+// each block takes a tile of whole rows holding <= kEvalTile entries, streams
+// the tile's (col, val) entries with coalesced loads (8 entries per thread in
+// flight), gathers w (L2-resident), parks the products in LDS, then 16-lane
+// groups (one DPP row each) sum the rows.  A row longer than a tile is summed
+// by the whole block.  The same launch sums alpha and ||w||^2.  Block partials
+// -> fixed-order final reduction (deterministic run to run).
 constexpr int kEvalBlock = 256;
-constexpr int kEvalMaxBlocks = 2048;
+constexpr int kEvalUnroll = 8;
+constexpr int kEvalBlocksPerCU = 6;  // 24 KB LDS per block
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    v = wave_sum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + red[2]) + red[3];
+}
 
 __global__ __launch_bounds__(kEvalBlock) void eval_fast_kernel(EvalArgs a) {
-    __shared__ double red[4][kEvalBlock / 64];
+    __shared__ double prod[kEvalTile];
+    __shared__ int32_t roff[kEvalTile + 1];
+    __shared__ double red[4];
     const int tid = threadIdx.x;
-    const int sub = tid & 15;
-    const int64_t ngroups = (int64_t)gridDim.x * (kEvalBlock / 16);
-    const int64_t g0 = (int64_t)blockIdx.x * (kEvalBlock / 16) + (tid >> 4);
-    const int64_t rows = a.n + a.n_test;
+    const int sub = tid & 15, grp = tid >> 4;
     double hinge = 0.0, err = 0.0;
-    for (int64_t r = g0; r < rows; r += ngroups) {
-        const bool test = r >= a.n;
-        const int64_t rr = test ? r - a.n : r;
+    const int64_t ntiles = a.n_tiles + a.n_t_tiles;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const bool test = t >= a.n_tiles;
+        const int64_t tt = test ? t - a.n_tiles : t;
+        const int64_t* tl = test ? a.t_tiles : a.tiles;
         const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
         const int32_t* cl = test ? a.t_col : a.col;
         const double* vl = test ? a.t_val : a.val;
-        const int64_t b = rp[rr], e = rp[rr + 1];
-        double acc0 = 0.0, acc1 = 0.0;
-        int64_t q = b + sub;
-        for (; q + 48 < e; q += 64) {
-            const int32_t c0 = cl[q], c1 = cl[q + 16], c2 = cl[q + 32], c3 = cl[q + 48];
-            const double v0 = vl[q], v1 = vl[q + 16], v2 = vl[q + 32], v3 = vl[q + 48];
-            acc0 += v0 * a.w[c0];
-            acc1 += v1 * a.w[c1];
-            acc0 += v2 * a.w[c2];
-            acc1 += v3 * a.w[c3];
+        const double* yy = test ? a.t_y : a.y;
+        const int64_t r0 = tl[tt], r1 = tl[tt + 1];
+        const int64_t e0 = rp[r0], e1 = rp[r1];
+        const int64_t T = e1 - e0;
+        if (T > kEvalTile) {
+            // one long row: the whole block reduces it
+            double acc = 0.0;
+            for (int64_t q = e0 + tid; q < e1; q += kEvalBlock) acc += vl[q] * a.w[cl[q]];
+            const double dot = block_sum(acc, red);
+            if (tid == 0) {
+                if (!test) hinge += jmax(1 - yy[r0] * dot, 0.0);
+                else err += (dot * yy[r0] > 0) ? 0.0 : 1.0;
+            }
+            continue;
         }
-        for (; q < e; q += 16) acc0 += vl[q] * a.w[cl[q]];
-        const double dot = row16_sum(acc0 + acc1);
-        if (sub == 0) {
-            if (!test)
-                hinge += jmax(1 - a.y[rr] * dot, 0.0);
-            else
-                err += (dot * a.t_y[rr] > 0) ? 0.0 : 1.0;
+        const int nr = (int)(r1 - r0);
+        for (int i = tid; i <= nr; i += kEvalBlock) roff[i] = (int32_t)(rp[r0 + i] - e0);
+        int32_t c[kEvalUnroll];
+        double v[kEvalUnroll];
+#pragma unroll
+        for (int u = 0; u < kEvalUnroll; ++u) {
+            const int64_t i = tid + (int64_t)u * kEvalBlock;
+            c[u] = 0;
+            v[u] = 0.0;
+            if (i < T) {
+                c[u] = cl[e0 + i];
+                v[u] = vl[e0 + i];
+            }
         }
+#pragma unroll
+        for (int u = 0; u < kEvalUnroll; ++u) {
+            const int64_t i = tid + (int64_t)u * kEvalBlock;
+            if (i < T) prod[i] = v[u] * a.w[c[u]];
+        }
+        __syncthreads();
+        for (int r = grp; r < nr; r += kEvalBlock / 16) {
+            const int32_t b = roff[r], e = roff[r + 1];
+            double acc = 0.0;
+            for (int32_t q = b + sub; q < e; q += 16) acc += prod[q];
+            const double dot = row16_sum(acc);
+            if (sub == 0) {
+                if (!test) hinge += jmax(1 - yy[r0 + r] * dot, 0.0);
+                else err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+            }
+        }
+        __syncthreads();
     }
     const int64_t gt = (int64_t)blockIdx.x * kEvalBlock + tid;
     const int64_t gs = (int64_t)gridDim.x * kEvalBlock;
     double al = 0.0, w2 = 0.0;
     for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
     for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
-    const double v[4] = {wave_sum(hinge), wave_sum(al), wave_sum(w2), wave_sum(err)};
-    if ((tid & 63) == 0)
-        for (int i = 0; i < 4; ++i) red[i][tid >> 6] = v[i];
-    __syncthreads();
-    if (tid < 4) {
-        double s = 0.0;
-        for (int wv = 0; wv < kEvalBlock / 64; ++wv) s += red[tid][wv];
-        a.partials[(size_t)blockIdx.x * 4 + tid] = s;
+    const double s0 = block_sum(hinge, red);
+    const double s1 = block_sum(al, red);
+    const double s2 = block_sum(w2, red);
+    const double s3 = block_sum(err, red);
+    if (tid == 0) {
+        double* p = a.partials + (size_t)blockIdx.x * 4;
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+        p[3] = s3;
     }
 }
 
@@ -84,10 +126,10 @@ __global__ __launch_bounds__(256) void eval_final_kernel(const double* partials,
     if (tid < 4) out[tid] = ((red[tid][0] + red[tid][1]) + red[tid][2]) + red[tid][3];
 }
 
-int eval_fast_blocks(int64_t n, int64_t n_test) {
-    const int64_t rows = n + n_test;
-    int64_t b = (rows + (kEvalBlock / 16) - 1) / (kEvalBlock / 16);
-    if (b > kEvalMaxBlocks) b = kEvalMaxBlocks;
+int eval_fast_blocks(int64_t n_tiles, int64_t n_t_tiles) {
+    int64_t b = n_tiles + n_t_tiles;
+    const int64_t cap = 256 * kEvalBlocksPerCU;
+    if (b > cap) b = cap;
     if (b < 1) b = 1;
     return (int)b;
 }

@@ -64,7 +64,7 @@ void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H,
 // round; then w += sum * mult (CoCoA.scala:48) or the sum is stored for an
 // external all-reduce.
 __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_t d, double* dw_sum, double* w,
-                                                   double mult, int apply) {
+                                                   double mult, int apply, const int32_t* inv) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
         double s = dw[j];
         dw[j] = 0.0;
@@ -76,25 +76,26 @@ __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_
         if (apply)
             w[j] = w[j] + (s * mult);
         else
-            dw_sum[j] = s;
+            dw_sum[inv ? inv[j] : j] = s;
     }
 }
 
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
-                 hipStream_t s) {
+                 const int32_t* inv, hipStream_t s) {
     int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
     if (blocks < 1) blocks = 1;
-    fold_kernel<<<blocks, 256, 0, s>>>(const_cast<double*>(dw), K, d, dw_sum, w, mult, apply ? 1 : 0);
+    fold_kernel<<<blocks, 256, 0, s>>>(const_cast<double*>(dw), K, d, dw_sum, w, mult, apply ? 1 : 0, inv);
 }
 
-__global__ __launch_bounds__(256) void apply_kernel(double* w, const double* dw_sum, int64_t d, double mult) {
+__global__ __launch_bounds__(256) void apply_kernel(double* w, const double* dw_sum, int64_t d, double mult,
+                                                    const int32_t* inv) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x)
-        w[j] = w[j] + (dw_sum[j] * mult);
+        w[j] = w[j] + (dw_sum[inv ? inv[j] : j] * mult);
 }
 
-void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, hipStream_t s) {
+void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const int32_t* inv, hipStream_t s) {
     int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
-    apply_kernel<<<blocks < 1 ? 1 : blocks, 256, 0, s>>>(w, dw_sum, d, mult);
+    apply_kernel<<<blocks < 1 ? 1 : blocks, 256, 0, s>>>(w, dw_sum, d, mult, inv);
 }
 
 __global__ __launch_bounds__(256) void scale_kernel(double* w, int64_t d, double scale) {
@@ -152,7 +153,10 @@ __global__ __launch_bounds__(1024) void eval_fold_strict(EvalArgs a) {
             }
         }
         double w2 = 0.0;
-        for (int64_t j = 0; j < a.d; ++j) w2 += a.w[j] * a.w[j];
+        for (int64_t j = 0; j < a.d; ++j) {  // index order of the original features
+            const double wj = a.w[a.perm ? a.perm[j] : j];
+            w2 += wj * wj;
+        }
         double err = 0.0;
         for (int64_t r = 0; r < a.n_test; ++r) err += a.row_scratch[a.n + r];
         a.out[0] = h;
