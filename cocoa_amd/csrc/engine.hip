@@ -485,9 +485,9 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     switch (method) {
         case COCOA_METHOD_COCOA_PLUS: ctx->scaling = params->gamma; break;       // CoCoA.scala:37
         case COCOA_METHOD_COCOA: ctx->scaling = params->beta / Kg; break;        // CoCoA.scala:37
-        case COCOA_METHOD_MBCD: ctx->scaling = params->beta / kh; break;         // MinibatchCD.scala:147
-        case COCOA_METHOD_LOCALSGD: ctx->scaling = params->beta / Kg; break;     // SGD.scala:285
-        case COCOA_METHOD_MBSGD: ctx->scaling = params->beta / kh; break;        // SGD.scala:287
+        case COCOA_METHOD_MBCD: ctx->scaling = params->beta / kh; break;         // MinibatchCD.scala:32
+        case COCOA_METHOD_LOCALSGD: ctx->scaling = params->beta / Kg; break;     // SGD.scala:36
+        case COCOA_METHOD_MBSGD: ctx->scaling = params->beta / kh; break;        // SGD.scala:38
     }
     hipStream_t s = ctx->stream;
     ctx->w.alloc(sizeof(double) * (size_t)d);
@@ -562,14 +562,14 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
                     launch_solver_fast(solver_mode(c->method), c->vec_lds, c->alpha_lds, c->sa, K, c->lds_bytes, s);
             });
         } else {
-            const double step = 1 / (c->P.lambda * (double)t);                 // SGD.scala:293
+            const double step = 1 / (c->P.lambda * (double)t);                 // SGD.scala:44
             const bool local = c->method == COCOA_METHOD_LOCALSGD;
             if (!local) {
-                const double scale = 1.0 - (step * c->P.lambda);             // SGD.scala:297-298
+                const double scale = 1.0 - (step * c->P.lambda);             // SGD.scala:48-49
                 c->timed(COCOA_K_APPLY, [&] { launch_scale(c->w.as<double>(), d, scale, s); });
-                c->mult = step * c->scaling;                                 // SGD.scala:307
+                c->mult = step * c->scaling;                                 // SGD.scala:58
             }
-            const double t0 = (double)wrap32((int64_t)(t - 1) * H * c->K_glob); // SGD.scala:302 (Int)
+            const double t0 = (double)wrap32((int64_t)(t - 1) * H * c->K_glob); // SGD.scala:53 (Int)
             c->timed(COCOA_K_SOLVER, [&] { launch_sgd(local, c->sa, c->P.lambda, t0, K, s); });
         }
     } else if (c->method == COCOA_METHOD_MBSGD) {

@@ -1,6 +1,6 @@
 // java.util.Random (the JDK's 48-bit LCG) for host and device, as drawn by
-// scala.util.Random(seed) in CoCoA.scala:144,151 (and MinibatchCD.scala:206,
-// SGD.scala:348).  The device sampler uses the affine jump-ahead
+// scala.util.Random(seed) in CoCoA.scala:144,151 (and MinibatchCD.scala:91,98,
+// SGD.scala:99,109).  The device sampler uses the affine jump-ahead
 //   s_{m+k} = A_k * s_m + C_k  (mod 2^48)
 // so that 256 threads draw consecutive raw values in parallel.
 #pragma once

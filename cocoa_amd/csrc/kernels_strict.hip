@@ -100,7 +100,7 @@ void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const
 
 __global__ __launch_bounds__(256) void scale_kernel(double* w, int64_t d, double scale) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x)
-        w[j] = w[j] * scale;  // w :*= scale (SGD.scala:298)
+        w[j] = w[j] * scale;  // w :*= scale (SGD.scala:49)
 }
 
 void launch_scale(double* w, int64_t d, double scale, hipStream_t s) {
@@ -174,7 +174,7 @@ void launch_eval_strict(const EvalArgs& a, hipStream_t s) {
 }
 
 // -------------------------------------------------------------- SGD (C5) --
-// SGD.partitionUpdate (SGD.scala:336-388), one workgroup per partition.
+// SGD.partitionUpdate (SGD.scala:87-139), one workgroup per partition.
 // mb-SGD: w is the driver's (already shrunk) w, read-only; deltaW accumulates
 // x*y over violators.  local-SGD: the task's copy w_loc is shrunk by
 // (1 - step*lambda) every step (O(d), as the reference does) and moved by
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(SolverArgs a, double lambda, d
         __syncthreads();
     }
     for (int32_t i = 1; i <= a.H; ++i) {
-        const double step = 1.0 / (lambda * (t0 + (double)i));         // SGD.scala:355
+        const double step = 1.0 / (lambda * (t0 + (double)i));         // SGD.scala:106
         const int32_t idx = a.samples[(size_t)k * a.H + (i - 1)];
         const int64_t gr = p0 + idx;
         const int64_t b = a.row_ptr[gr], e = a.row_ptr[gr + 1];
@@ -204,16 +204,16 @@ __global__ __launch_bounds__(256) void sgd_kernel(SolverArgs a, double lambda, d
             double s = 0.0;
             if (lane == 0)
                 for (int64_t q = b; q < e; ++q) s += a.val[q] * wl[a.col[q]];
-            if (lane == 0) sh_eval = 1.0 - (yv * (s));                    // SGD.scala:364
+            if (lane == 0) sh_eval = 1.0 - (yv * (s));                    // SGD.scala:115
         }
         __syncthreads();
         const double ev = sh_eval;
         if (LOCAL) {
-            const double scale = 1.0 - (step * lambda);                  // SGD.scala:368-369
+            const double scale = 1.0 - (step * lambda);                  // SGD.scala:119-120
             for (int64_t j = tid; j < d; j += 256) wl[j] = wl[j] * scale;
             __syncthreads();
         }
-        if (ev > 0) {                                                    // SGD.scala:373-379
+        if (ev > 0) {                                                    // SGD.scala:124-130
             if (tid == 0) {
                 for (int64_t q = b; q < e; ++q) {
                     const double u = a.val[q] * yv;
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(SolverArgs a, double lambda, d
         __syncthreads();
     }
     if (LOCAL)
-        for (int64_t j = tid; j < d; j += 256) dwk[j] = wl[j] - a.w[j];  // deltaW = w - wInit (SGD.scala:382)
+        for (int64_t j = tid; j < d; j += 256) dwk[j] = wl[j] - a.w[j];  // deltaW = w - wInit (SGD.scala:133)
     (void)red;
 }
 

@@ -7,7 +7,7 @@
 //            x_i.w in stored-entry order.
 //   wave 0 = solver: the strictly sequential chain of H coordinate steps of
 //            CoCoA.localSDCA (CoCoA.scala:148-188) / MinibatchCD
-//            (MinibatchCD.scala:210-240), reading its rows from LDS.  The only
+//            (MinibatchCD.scala:95-125), reading its rows from LDS.  The only
 //            memory it waits on per step is the gather of the mutable vector
 //            (deltaW for CoCoA+, the task's w copy for CoCoA), which lives in
 //            LDS when d fits, else in a private HBM/L2 slice.
@@ -250,7 +250,7 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
         else if (MODE == MODE_COCOA)
             grad = (yv * (sdot) - 1.0) * lam_n;                  // CoCoA.scala:161
         else
-            grad = (yv * (xw) - 1.0) * lam_n;                    // MinibatchCD.scala:219
+            grad = (yv * (xw) - 1.0) * lam_n;                    // MinibatchCD.scala:104
         double proj = grad;                                      // CoCoA.scala:166-170
         if (aa <= 0.0)
             proj = jmin(grad, 0.0);
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
         for (int i = 0; i < 6; ++i) pr[3 + i] = step_prof[i];
     }
     // epilogue: alpha = alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101,
-    // MinibatchCD.scala:242-243)
+    // MinibatchCD.scala:127-128)
     if (a.raw_alpha) {
         for (int32_t i = tid; i < nl; i += 128) a.alpha[p0 + i] = alv[i];
         if (VEC_LDS && MODE == MODE_COCOA)

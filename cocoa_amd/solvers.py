@@ -135,7 +135,7 @@ class SGD:
     @staticmethod
     def runSGD(data, params, debug, local, strict=False, device=0, printer=None):
         p = printer or _Printer.out
-        # SGD.scala:27 prints its own banner
+        # SGD.scala:29 prints its own banner
         name = f"SGD (with local updates = {'true' if local else 'false'})"
         w, _ = _run("localsgd" if local else "mbsgd", name, data, params, debug, strict, device, False,
                     lambda s: p(s))

@@ -112,8 +112,8 @@ int cocoa_set_test(cocoa_ctx *ctx, const int64_t *row_ptr, const int32_t *col, c
  * hingeDriver.scala:75), scaling per method (CoCoA.scala:37). */
 int cocoa_init(cocoa_ctx *ctx, const cocoa_params *params, const cocoa_debug *debug, int method, const double *w_init);
 /* Round t (1-based), local half: sampling with seed+t, K local solvers
- * (CoCoA.localSDCA, CoCoA.scala:130-192 / MinibatchCD.scala:200-240 /
- * SGD.scala:336-388), alpha update (CoCoA.scala:101) and this rank's ordered
+ * (CoCoA.localSDCA, CoCoA.scala:130-192 / MinibatchCD.scala:76-132 /
+ * SGD.scala:87-139), alpha update (CoCoA.scala:101) and this rank's ordered
  * deltaW fold into the device buffer returned by cocoa_dw_sum_device_ptr. */
 int cocoa_round_local(cocoa_ctx *ctx, int32_t t);
 /* Device pointer (double[num_features]) holding this rank's deltaW sum after
@@ -122,8 +122,8 @@ int cocoa_dw_sum_device_ptr(cocoa_ctx *ctx, void **out);
 /* Redirect the deltaW sum into caller-owned device memory (e.g. a tensor
  * that torch.distributed all-reduces).  NULL restores the internal buffer. */
 int cocoa_set_dw_sum_buffer(cocoa_ctx *ctx, void *device_ptr);
-/* w += sum * scaling (CoCoA.scala:47-48; MinibatchCD.scala:157-158;
- * SGD.scala:303-308). */
+/* w += sum * scaling (CoCoA.scala:47-48; MinibatchCD.scala:42-43;
+ * SGD.scala:54-59). */
 int cocoa_round_apply(cocoa_ctx *ctx);
 /* One full round on a single rank = local + apply. */
 int cocoa_round(cocoa_ctx *ctx, int32_t t);

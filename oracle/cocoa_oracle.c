@@ -38,7 +38,7 @@
 
 /* ------------------------------------------------------------------------- */
 /* java.util.Random, as used by scala.util.Random(seed: Int)                  */
-/* (CoCoA.scala:144,151; MinibatchCD.scala:206,213; SGD.scala:348,358).       */
+/* (CoCoA.scala:144,151; MinibatchCD.scala:91,98; SGD.scala:99,109).            */
 /* JDK algorithm: 48-bit LCG, multiplier 0x5DEECE66D, addend 0xB.             */
 /* ------------------------------------------------------------------------- */
 #define JR_MULT 0x5DEECE66DULL
@@ -384,7 +384,7 @@ void oracle_local_sdca(const int64_t *row_ptr, const int32_t *col, const double 
         for (int32_t i = 0; i < n_local; ++i) delta_alpha[i] = alpha[i] - alpha_old[i];
 }
 
-/* MinibatchCD.partitionUpdate inner loop (MinibatchCD.scala:200-240): like
+/* MinibatchCD.partitionUpdate inner loop (MinibatchCD.scala:76-132): like
  * !plus localSDCA but with the stale w (never written) and no sigma. */
 static void mbcd_local(const int64_t *row_ptr, const int32_t *col, const double *val, const double *y, int32_t n_local,
                        int32_t d, const double *w, int32_t local_iters, double lambda, int32_t n, double *alpha,
@@ -553,7 +553,7 @@ oracle_run *oracle_run_create(const oracle_data *train, int method, int32_t n, i
 }
 
 /* scaling per method from the GLOBAL partition count (CoCoA.scala:37,
- * MinibatchCD.scala:147, SGD.scala:283-288) */
+ * MinibatchCD.scala:32, SGD.scala:34-39) */
 void oracle_run_set_scaling(oracle_run *R) {
     const int64_t K = R->Kg;
     const int32_t H = R->H;
@@ -564,9 +564,9 @@ void oracle_run_set_scaling(oracle_run *R) {
     switch (method) {
         case M_PLUS: R->scaling = gamma; break;                       /* CoCoA.scala:37 */
         case M_COCOA: R->scaling = beta / (double)K; break;           /* CoCoA.scala:37 */
-        case M_MBCD: R->scaling = beta / kh; break;                   /* MinibatchCD.scala:147 */
-        case M_LOCALSGD: R->scaling = beta / (double)K; break;        /* SGD.scala:285 */
-        case M_MBSGD: R->scaling = beta / kh; break;                  /* SGD.scala:287 */
+        case M_MBCD: R->scaling = beta / kh; break;                   /* MinibatchCD.scala:32 */
+        case M_LOCALSGD: R->scaling = beta / (double)K; break;        /* SGD.scala:36 */
+        case M_MBSGD: R->scaling = beta / kh; break;                  /* SGD.scala:38 */
     }
 }
 
@@ -633,7 +633,7 @@ void oracle_run_local(oracle_run *R, int32_t t, double *dw_sum) {
     int64_t d = D->d;
     double t0 = 0.0;
     if (R->method == M_MBSGD || R->method == M_LOCALSGD) {
-        double step = 1 / (R->lambda * (double)t);                    /* SGD.scala:293 */
+        double step = 1 / (R->lambda * (double)t);                    /* SGD.scala:44 */
         R->sgd_step = step;
         if (R->method == M_MBSGD) {                                   /* :295-299 */
             double scale = 1.0 - (step * R->lambda);
@@ -661,7 +661,7 @@ void oracle_run_local(oracle_run *R, int32_t t, double *dw_sum) {
     }
     /* reduce(_ + _) in partition order (CoCoA.scala:47) */
     R->mult = R->scaling;
-    if (R->method == M_MBSGD) R->mult = R->sgd_step * R->scaling;    /* SGD.scala:307 */
+    if (R->method == M_MBSGD) R->mult = R->sgd_step * R->scaling;    /* SGD.scala:58 */
     for (int64_t j = 0; j < d; ++j) {
         double s = 0.0;
         int have = 0;
