@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -125,10 +126,16 @@ struct cocoa_ctx {
     double* h_eval = nullptr;  // pinned [4]
     int64_t samples_cap = 0;
 
-    // solver plan
+    // solver plan (v1: CoCoA, unit fallbacks)
     bool vec_lds = false, alpha_lds = false;
     size_t lds_bytes = 0;
     SolverArgs sa{};
+    // solver plan (v2: CoCoA+ / MbCD)
+    bool use_v2 = false;
+    size_t lds2_bytes = 0;
+    Solver2Args sa2{};
+    DevBuf plan_beg, plan_z, plan_y, plan_q, plan_xw;
+    int32_t max_z = 0;
 
     // stats
     bool stats = false;
@@ -342,6 +349,8 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     std::vector<double> sq((size_t)std::max<int64_t>(n_rows, 1));
     std::vector<uint8_t> fl((size_t)std::max<int64_t>(n_rows, 1), 0);
     ctx->any_dup = false;
+    ctx->max_z = 0;
+    for (int64_t r = 0; r < n_rows; ++r) ctx->max_z = (int32_t)std::max<int64_t>(ctx->max_z, row_ptr[r + 1] - row_ptr[r]);
     std::vector<int64_t> seen_at((size_t)num_features, -1);
     for (int64_t r = 0; r < n_rows; ++r) {
         double s = 0.0;
@@ -466,6 +475,88 @@ static void plan_solver(cocoa_ctx* c) {
     a.stream_cap = (int32_t)cap;
 }
 
+static size_t pow2_at_least(size_t x) {
+    size_t p = 32;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// LDS carve of the v2 solver: hot deltaW slice + double-buffered (col, val,
+// cold) streams + batch metadata + dirty bitmaps.  All of d goes to LDS when
+// it fits (then no cold stream); otherwise the hot slice takes what is left
+// after a 1024-entry stream.
+static void plan_solver2(cocoa_ctx* c, int32_t max_nl) {
+    Solver2Args& a = c->sa2;
+    const size_t budget = kLdsMax;
+    const size_t meta = 2 * align16(sizeof(Batch2));
+    const size_t scratch = align16(sizeof(double) * kRegChunks * 64) + 64 * sizeof(double);  // + sink
+    const size_t nb_a = std::min<size_t>(pow2_at_least((size_t)std::max(max_nl, 1)), 65536);
+    const size_t abytes = 2 * align16(nb_a / 8);
+    const size_t d = (size_t)c->d;
+    size_t hot, cap, nb_w;
+    bool cold;
+    const size_t fixed_nocold = meta + scratch + abytes + 2 * align16(4);
+    if (align16(d * 8) + fixed_nocold + 2 * 1024 * 12 <= budget) {
+        cold = false;
+        hot = d;
+        nb_w = 32;
+        cap = (budget - align16(d * 8) - fixed_nocold) / 24;   // 2 buffers x (4 + 8) B
+        cap = std::min<size_t>(cap & ~(size_t)63, 8192);
+        cap = std::max<size_t>(cap, (size_t)std::min<int32_t>(c->max_z, 8192) & ~(size_t)63);
+        while (align16(d * 8) + fixed_nocold + 2 * (align16(cap * 4) + align16(cap * 8)) > budget) cap -= 64;
+    } else {
+        cold = true;
+        cap = 1024;
+        const size_t fixed = meta + scratch + abytes + 2 * (align16(cap * 4) + 2 * align16(cap * 8));
+        nb_w = std::min<size_t>(pow2_at_least(d), 65536);
+        for (int it = 0; it < 3; ++it) {
+            hot = (budget - fixed - 2 * align16(nb_w / 8)) / 8;
+            hot &= ~(size_t)15;
+            hot = std::min(hot, d);
+            nb_w = std::min<size_t>(pow2_at_least(d - hot), 65536);
+        }
+        hot = (budget - fixed - 2 * align16(nb_w / 8)) / 8;
+        hot = std::min(hot & ~(size_t)15, d);
+    }
+    size_t off = 0;
+    a.lds_hot = (int32_t)off;
+    off += align16(hot * 8);
+    for (int b = 0; b < 2; ++b) {
+        a.lds_dirty_w[b] = (int32_t)off;
+        off += align16(nb_w / 8);
+        a.lds_dirty_a[b] = (int32_t)off;
+        off += align16(nb_a / 8);
+        a.lds_col[b] = (int32_t)off;
+        off += align16(cap * 4);
+        a.lds_val[b] = (int32_t)off;
+        off += align16(cap * 8);
+        if (cold) {
+            a.lds_cold[b] = (int32_t)off;
+            off += align16(cap * 8);
+        } else {
+            a.lds_cold[b] = -1;
+        }
+        a.lds_batch[b] = (int32_t)off;
+        off += align16(sizeof(Batch2));
+    }
+    a.lds_scratch = (int32_t)off;
+    a.lds_sink = (int32_t)(off + align16(sizeof(double) * kRegChunks * 64));
+    off += scratch;
+    if (off > budget) throw Error(COCOA_E_ARG, "v2 solver LDS plan exceeds 160 KiB");
+    a.hot = (int32_t)hot;
+    a.cap = (int32_t)cap;
+    a.wmask = (int32_t)(nb_w - 1);
+    a.amask = (int32_t)(nb_a - 1);
+    c->lds2_bytes = off;
+}
+
+// v2 is opt-in (COCOA_SOLVER=v2): on C2 it measured 10.5 ms/round against
+// v1's 9.8 ms (profiles/r01_bench_v2.json), so v1 stays the default.
+static bool v2_enabled() {
+    const char* e = std::getenv("COCOA_SOLVER");
+    return e && std::strcmp(e, "v2") == 0;
+}
+
 extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
                           const double* w_init) {
     CAPI_BEGIN(ctx)
@@ -537,6 +628,47 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.lam_n = params->lambda * (double)params->n;
     a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
     a.scaling = ctx->scaling;
+
+    ctx->use_v2 = v2_enabled() && (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_MBCD);
+    if (ctx->use_v2) {
+        const size_t steps = (size_t)std::max<int64_t>((int64_t)K * H, 1);
+        ctx->plan_beg.alloc(steps * sizeof(int64_t));
+        ctx->plan_z.alloc(steps * sizeof(int32_t));
+        ctx->plan_y.alloc(steps * sizeof(double));
+        ctx->plan_q.alloc(steps * sizeof(double));
+        ctx->plan_xw.alloc(steps * sizeof(double));
+        plan_solver2(ctx, ctx->max_nl);
+        Solver2Args& b = ctx->sa2;
+        b.row_ptr = a.row_ptr;
+        b.col = a.col;
+        b.val = a.val;
+        b.rowflags = a.rowflags;
+        b.part_ptr = a.part_ptr;
+        b.samples = a.samples;
+        b.plan_beg = ctx->plan_beg.as<int64_t>();
+        b.plan_z = ctx->plan_z.as<int32_t>();
+        b.plan_y = ctx->plan_y.as<double>();
+        b.plan_q = ctx->plan_q.as<double>();
+        b.plan_xw = ctx->plan_xw.as<double>();
+        b.alpha = a.alpha;
+        b.alpha_work = a.alpha_work;
+        b.dw = a.dw;
+        b.d = d;
+        b.H = H;
+        b.any_dup = a.any_dup;
+        b.raw_alpha = 0;
+        b.dbg_serial = std::getenv("COCOA_DBG_SERIAL") ? 1 : 0;
+        b.lam_n = a.lam_n;
+        b.sigma = a.sigma;
+        b.scaling = a.scaling;
+        b.prof = nullptr;
+    } else {
+        ctx->plan_beg.free();
+        ctx->plan_z.free();
+        ctx->plan_y.free();
+        ctx->plan_q.free();
+        ctx->plan_xw.free();
+    }
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = true;
     CAPI_END(ctx)
@@ -554,7 +686,37 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         c->timed(COCOA_K_SAMPLE, [&] {
             launch_sampler(c->part_ptr.as<int64_t>(), K, seed, H, c->samples.as<int32_t>(), c->jump.as<uint64_t>(), s);
         });
-        if (is_sdca(c->method)) {
+        if (c->use_v2) {
+            PlanArgs pa{};
+            pa.part_ptr = c->part_ptr.as<int64_t>();
+            pa.samples = c->samples.as<int32_t>();
+            pa.row_ptr = c->tr.row_ptr.as<int64_t>();
+            pa.col = c->tr.col.as<int32_t>();
+            pa.val = c->tr.val.as<double>();
+            pa.y = c->tr.y.as<double>();
+            pa.sqn = c->sqn.as<double>();
+            pa.w = c->w.as<double>();
+            pa.steps = (int64_t)K * H;
+            pa.H = H;
+            pa.need_xw = 1;
+            pa.beg = c->plan_beg.as<int64_t>();
+            pa.z = c->plan_z.as<int32_t>();
+            pa.py = c->plan_y.as<double>();
+            pa.pq = c->plan_q.as<double>();
+            pa.xw = c->plan_xw.as<double>();
+            c->timed(COCOA_K_PLAN, [&] {
+                if (c->strict)
+                    launch_plan_strict(pa, s);
+                else
+                    launch_plan_fast(pa, s);
+            });
+            c->timed(COCOA_K_SOLVER, [&] {
+                if (c->strict)
+                    launch_solver2_strict(solver_mode(c->method), c->sa2, K, c->lds2_bytes, s);
+                else
+                    launch_solver2_fast(solver_mode(c->method), c->sa2, K, c->lds2_bytes, s);
+            });
+        } else if (is_sdca(c->method)) {
             c->timed(COCOA_K_SOLVER, [&] {
                 if (c->strict)
                     launch_solver_strict(solver_mode(c->method), c->vec_lds, c->alpha_lds, c->sa, K, c->lds_bytes, s);
@@ -873,8 +1035,10 @@ extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
     if (enable) {
         ctx->prof.alloc_zero(sizeof(uint64_t) * (size_t)ctx->K_loc * 32, ctx->stream);
         ctx->sa.prof = ctx->prof.as<uint64_t>();
+        ctx->sa2.prof = ctx->prof.as<uint64_t>();
     } else {
         ctx->sa.prof = nullptr;
+        ctx->sa2.prof = nullptr;
     }
     CAPI_END(ctx)
 }
@@ -893,8 +1057,14 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
     require(buf && len > 0, COCOA_E_ARG, "bad buffer");
     std::snprintf(buf, (size_t)len,
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
-                  "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d}",
+                  "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,\"solver\":\"%s\","
+                  "\"hot\":%d,\"cap2\":%d,\"lds2_bytes\":%zu,\"hot_nnz_frac\":%.4f}",
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
-                  ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl);
+                  ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
+                  ctx->use_v2 ? "v2" : "v1", ctx->use_v2 ? ctx->sa2.hot : 0, ctx->use_v2 ? ctx->sa2.cap : 0,
+                  ctx->lds2_bytes,
+                  ctx->use_v2 && ctx->tr.nnz > 0
+                      ? (double)ctx->n_hot_nnz[(size_t)ctx->sa2.hot] / (double)ctx->tr.nnz
+                      : 0.0);
     CAPI_END(ctx)
 }

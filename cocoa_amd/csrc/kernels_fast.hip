@@ -2,6 +2,7 @@
 // fused multiply-adds.  Results agree with the strict path within the 1e-9
 // relative tolerance of BASELINE.json's north_star.
 #include "kernels.h"
+#include "solver2_impl.h"
 #include "solver_impl.h"
 #include "wave.h"
 
@@ -11,6 +12,12 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
                         hipStream_t s) {
     launch_solver_impl<false>(mode, vec_lds, alpha_lds, a, grid, lds, s);
 }
+
+void launch_solver2_fast(int mode, const Solver2Args& a, int grid, size_t lds, hipStream_t s) {
+    launch_solver2_impl<false>(mode, a, grid, lds, s);
+}
+
+void launch_plan_fast(const PlanArgs& a, hipStream_t s) { launch_plan_impl<false>(a, s); }
 
 // ----------------------------------------------------------- fused eval --
 // One pass over train + test CSR (OptUtils.scala:57-98) as a CSR stream:

@@ -165,7 +165,8 @@ int cocoa_samples(cocoa_ctx *ctx, int32_t part, int32_t seed_plus_t, int32_t cou
 #define COCOA_K_FOLD 2
 #define COCOA_K_APPLY 3
 #define COCOA_K_EVAL 4
-#define COCOA_K_COUNT 5
+#define COCOA_K_PLAN 5   /* per-round step plan (row offsets, x.w) of the v2 solver */
+#define COCOA_K_COUNT 6
 /* enable = 1: bracket every launch with HIP events on the context stream. */
 int cocoa_stats_enable(cocoa_ctx *ctx, int enable);
 /* total device milliseconds and launch count per kernel id since last reset */

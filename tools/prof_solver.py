@@ -39,6 +39,7 @@ def main():
         p = e.solver_profile_read().astype(np.float64)
         st = e.kernel_stats()
         comp, load = p[:, 0, :], p[:, 1, :]
+        e.stats_reset()
         rec = {"t": t, "solver_ms_total": st["solver"]["total_ms"],
                "compute_busy_cyc_mean": comp[:, 0].mean(), "compute_wait_cyc_mean": comp[:, 1].mean(),
                "loader_busy_cyc_mean": load[:, 0].mean(), "loader_wait_cyc_mean": load[:, 1].mean(),
@@ -46,7 +47,7 @@ def main():
                "cyc_per_step_compute": comp[:, 0].mean() / H, "cyc_per_step_total": (comp[:, 0] + comp[:, 1]).mean() / H,
                "step_phase_cyc_per_step": (comp[:, 3:9].mean(axis=0) / H).tolist()}
         out.append(rec)
-    print(json.dumps({"lib": os.environ.get("COCOA_LIB", "default"), "plan": e.plan(), "H": H, "records": out}))
+    print(json.dumps({"lib": os.environ.get("COCOA_LIB", "default"), "tag": "serial" if os.environ.get("COCOA_DBG_SERIAL") else "overlap", "plan": e.plan(), "H": H, "records": out}))
 
 
 if __name__ == "__main__":
