@@ -165,13 +165,25 @@ def main():
     solver_ms = stats["solver"]["total_ms"] / max(stats["solver"]["launches"], 1)
     b_solver = np.mean([solver_bytes_per_round(tr, H, t_ + 0) for t_ in timed_rounds[:4]])
     ach = b_solver / (solver_ms * 1e-3) / 1e9
-    traffic = None
+    # HBM traffic per launch from the committed PMC passes (tools/gpu_pmc.sh ->
+    # tools/pmc_summary.py -> profiles/traffic.json), used only when the PMC run
+    # profiled the same kernel variant this run launched
+    plan = eng.plan()
+    solver_tag = "solver2_kernel" if plan.get("solver") == "v2" else "solver_kernel<"
+    eval_tag = {"v1": "eval_fast_kernel", "v2": "eval_pf_kernel<1024", "v3": "eval_pf_kernel<256"}[
+        os.environ.get("COCOA_EVAL", "v1") if os.environ.get("COCOA_EVAL", "v1") in ("v1", "v2", "v3") else "v1"]
+    traffic = traffic_eval = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf):
+    if os.path.exists(tf) and not args.strict:
         try:
-            traffic = json.load(open(tf)).get("solver_bytes_per_launch")
+            tk = json.load(open(tf)).get("kernels", {})
+            for rec in tk.values():
+                if solver_tag in rec["kernel"] and "<0, false" in rec["kernel"].replace("cocoa::", ""):
+                    traffic = rec["hbm_bytes_per_launch"]
+                if eval_tag in rec["kernel"]:
+                    traffic_eval = rec["hbm_bytes_per_launch"]
         except Exception:
-            traffic = None
+            traffic = traffic_eval = None
     eval_ms = stats["eval"]["total_ms"] / max(stats["eval"]["launches"], 1)
     b_eval = (12 * tr.nnz + 8 * (tr.n + 1) + 8 * tr.n + 8 * tr.n + 8 * args.d
               + 12 * te.nnz + 8 * (te.n + 1) + 8 * te.n)
@@ -217,10 +229,10 @@ def main():
                          "note": "latency-bound sequential chain (H dependent steps per partition)"},
             "roofline_eval": {"kernel": "eval (primal/dual/gap/test error SpMV)", "bound": "hbm", "achieved": ach_eval,
                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach_eval / PEAK_HBM_GBS,
-                              "bytes_per_launch": b_eval, "avg_launch_ms": eval_ms},
+                              "traffic": traffic_eval, "bytes_per_launch": b_eval, "avg_launch_ms": eval_ms},
             "kernel_ms": {k: (v["total_ms"] / max(v["launches"], 1)) for k, v in stats.items()},
             "cpu_baseline": cpu,
-            "plan": eng.plan(),
+            "plan": plan,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -301,9 +301,13 @@ static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStr
         }
         t.push_back(r);
     }
+    // second half: entry offset of every tile boundary, so a tile's extent is
+    // four independent loads (no row_ptr round trip before the data loads)
+    const size_t nb = t.size();
+    for (size_t i = 0; i < nb; ++i) t.push_back(row_ptr[t[i]]);
     upload(out, t.data(), sizeof(int64_t) * t.size(), s);
     HIPCHK(hipStreamSynchronize(s));
-    return (int64_t)t.size() - 1;
+    return (int64_t)nb - 1;
 }
 
 static void check_csr(const int64_t* row_ptr, const int32_t* col, int64_t n, int32_t d) {
@@ -550,8 +554,24 @@ static void plan_solver2(cocoa_ctx* c, int32_t max_nl) {
     c->lds2_bytes = off;
 }
 
+// fast eval kernel: COCOA_EVAL=v1 (tile stream; default), v2 (hot w in LDS +
+// tile prefetch, one block per CU), v3 (tile prefetch, 6 blocks per CU).
+// Measured on C2 (r01): v1 0.238 ms, v2 0.320 ms, v3 0.274 ms.
+static int eval_version() {
+    const char* e = std::getenv("COCOA_EVAL");
+    if (e && std::strcmp(e, "v2") == 0) return 2;
+    if (e && std::strcmp(e, "v3") == 0) return 3;
+    return 1;
+}
+
 // v2 is opt-in (COCOA_SOLVER=v2): on C2 it measured 10.5 ms/round against
 // v1's 9.8 ms (profiles/r01_bench_v2.json), so v1 stays the default.
+// fast CoCoA+/MbCD step chain: v3 (pipelined, branch-free) unless COCOA_CHAIN=v1
+static int chain_version() {
+    const char* e = std::getenv("COCOA_CHAIN");
+    return (e && std::strcmp(e, "v1") == 0) ? 1 : 3;
+}
+
 static bool v2_enabled() {
     const char* e = std::getenv("COCOA_SOLVER");
     return e && std::strcmp(e, "v2") == 0;
@@ -624,6 +644,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.H = H;
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 0;
+    a.chain = chain_version();
     a.prof = nullptr;
     a.lam_n = params->lambda * (double)params->n;
     a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
@@ -829,8 +850,10 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     ctx->timed(COCOA_K_EVAL, [&] {
         if (ctx->strict)
             launch_eval_strict(e, ctx->stream);
-        else
+        else if (eval_version() == 1)
             launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
+        else
+            launch_eval2(eval_version(), e, eval2_blocks(eval_version(), e.n_tiles, e.n_t_tiles), ctx->stream);
     });
     HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -962,6 +985,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     a.H = local_iters;
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 1;
+    a.chain = chain_version();
     a.prof = nullptr;
     a.lam_n = lambda * (double)n;
     a.sigma = sigma;

@@ -27,6 +27,7 @@ struct BatchMeta {
     double y[kMetaSteps];      // label
     double q[kMetaSteps];      // Math.pow(norm(x), 2)
     double xw[kMetaSteps];     // x . w (read-only w: CoCoA+ and MbCD), summed in stored order
+    double rq[kMetaSteps];     // fast mode: 1 / qii, so the chain multiplies instead of dividing
     int32_t m;                 // steps in this batch (0 = no more work)
     int32_t pad[3];
 };
@@ -50,6 +51,8 @@ struct SolverArgs {
     int32_t stream_cap;       // staged entries per batch buffer
     int32_t any_dup;
     int32_t raw_alpha;        // 1: write the raw local alpha (unit localSDCA API)
+    int32_t chain;            // fast CoCoA+/MbCD: 3 = pipelined branch-free step chain, 1 = v1 chain
+    int32_t pad0;
     double lam_n;             // lambda * n
     double sigma;             // sigma' = K * gamma (CoCoA+)
     double scaling;           // alpha <- alphaOld + dAlpha * scaling
@@ -176,6 +179,8 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
                         hipStream_t s);
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
 int eval_fast_blocks(int64_t n, int64_t n_test);
+void launch_eval2(int version, const EvalArgs& a, int blocks, hipStream_t s);
+int eval2_blocks(int version, int64_t n, int64_t n_test);
 
 void launch_solver2_fast(int mode, const Solver2Args& a, int grid, size_t lds, hipStream_t s);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);

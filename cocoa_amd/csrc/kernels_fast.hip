@@ -51,12 +51,13 @@ __global__ __launch_bounds__(kEvalBlock) void eval_fast_kernel(EvalArgs a) {
         const bool test = t >= a.n_tiles;
         const int64_t tt = test ? t - a.n_tiles : t;
         const int64_t* tl = test ? a.t_tiles : a.tiles;
+        const int64_t* te = tl + (test ? a.n_t_tiles : a.n_tiles) + 1;  // entry offsets of the boundaries
         const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
         const int32_t* cl = test ? a.t_col : a.col;
         const double* vl = test ? a.t_val : a.val;
         const double* yy = test ? a.t_y : a.y;
         const int64_t r0 = tl[tt], r1 = tl[tt + 1];
-        const int64_t e0 = rp[r0], e1 = rp[r1];
+        const int64_t e0 = te[tt], e1 = te[tt + 1];
         const int64_t T = e1 - e0;
         if (T > kEvalTile) {
             // one long row: the whole block reduces it
@@ -119,6 +120,159 @@ __global__ __launch_bounds__(kEvalBlock) void eval_fast_kernel(EvalArgs a) {
     }
 }
 
+// Eval v2/v3: the (col, val, row_ptr) loads of a block's next tile are issued
+// before the current tile's row sums, so one tile of HBM reads is always in
+// flight behind the LDS work.  Same tiles, same per-row 16-lane DPP sums and
+// the same fixed-order block partials as eval v1.
+//   WLDS (v2): one 1024-thread block per CU that first copies the hot head of
+//              w (device feature order = descending frequency) into LDS;
+//   v3:        256-thread blocks, several per CU, w gathered from L1/L2.
+constexpr int kEvalHotW = 16384;  // doubles of w staged in LDS by v2 (128 KiB)
+constexpr int kEval3BlocksPerCU = 6;
+
+template <int BLOCK>
+struct EvalTileRegs {
+    static constexpr int PER = kEvalTile / BLOCK;            // entries per thread
+    static constexpr int RO = (kEvalTile + 1 + BLOCK - 1) / BLOCK;  // row offsets per thread
+    int64_t r0 = 0, e0 = 0, T = -1;  // T < 0: no tile
+    int32_t nr = 0;
+    bool test = false, longrow = false;
+    int32_t c[PER];
+    double v[PER];
+    int32_t ro[RO];
+};
+
+template <int BLOCK>
+__device__ __forceinline__ void eval_fetch(const EvalArgs& a, int64_t t, int64_t ntiles, EvalTileRegs<BLOCK>& x) {
+    using R = EvalTileRegs<BLOCK>;
+    const int tid = threadIdx.x;
+    x.T = -1;
+    if (t >= ntiles) return;
+    x.test = t >= a.n_tiles;
+    const int64_t tt = x.test ? t - a.n_tiles : t;
+    const int64_t* tl = x.test ? a.t_tiles : a.tiles;
+    const int64_t* te = tl + (x.test ? a.n_t_tiles : a.n_tiles) + 1;
+    const int64_t* rp = x.test ? a.t_row_ptr : a.row_ptr;
+    const int32_t* cl = x.test ? a.t_col : a.col;
+    const double* vl = x.test ? a.t_val : a.val;
+    const int64_t r0 = tl[tt], r1 = tl[tt + 1];
+    const int64_t e0 = te[tt], e1 = te[tt + 1];
+    x.r0 = r0;
+    x.e0 = e0;
+    x.T = e1 - e0;
+    x.nr = (int32_t)(r1 - r0);
+    x.longrow = x.T > kEvalTile;
+    if (x.longrow) return;
+#pragma unroll
+    for (int u = 0; u < R::PER; ++u) {
+        const int64_t i = tid + (int64_t)u * BLOCK;
+        x.c[u] = 0;
+        x.v[u] = 0.0;
+        if (i < x.T) {
+            x.c[u] = __builtin_nontemporal_load(cl + e0 + i);
+            x.v[u] = __builtin_nontemporal_load(vl + e0 + i);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < R::RO; ++u) {
+        const int i = tid + u * BLOCK;
+        x.ro[u] = i <= x.nr ? (int32_t)(rp[r0 + i] - e0) : 0;
+    }
+}
+
+template <int BLOCK>
+__device__ __forceinline__ double block_sum_n(double v, double* red) {
+    v = wave_sum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int i = 0; i < BLOCK / 64; ++i) s += red[i];
+    return s;
+}
+
+template <int BLOCK, bool WLDS>
+__global__ __launch_bounds__(BLOCK) void eval_pf_kernel(EvalArgs a) {
+    using R = EvalTileRegs<BLOCK>;
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    double* wh = (double*)lds;                                  // [kEvalHotW] (WLDS)
+    double* prod = wh + (WLDS ? kEvalHotW : 0);                 // [kEvalTile]
+    int32_t* roff = (int32_t*)(prod + kEvalTile);               // [kEvalTile + 1] (+pad)
+    double* red = (double*)(roff + kEvalTile + 4);              // [BLOCK / 64]
+    const int tid = threadIdx.x;
+    const int sub = tid & 15, grp = tid >> 4;
+    const int hw = WLDS ? (int)(a.d < kEvalHotW ? a.d : kEvalHotW) : 0;
+    if (WLDS)
+        for (int j = tid; j < hw; j += BLOCK) wh[j] = a.w[j];
+    auto wv = [&](int32_t c) { return (WLDS && c < hw) ? wh[c] : a.w[c]; };
+    double hinge = 0.0, err = 0.0;
+    const int64_t ntiles = a.n_tiles + a.n_t_tiles;
+    R cur, nxt;
+    eval_fetch<BLOCK>(a, blockIdx.x, ntiles, cur);
+    if (WLDS) __syncthreads();
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (cur.longrow) {
+            const int64_t* rp = cur.test ? a.t_row_ptr : a.row_ptr;
+            const int32_t* cl = cur.test ? a.t_col : a.col;
+            const double* vl = cur.test ? a.t_val : a.val;
+            const double* yy = cur.test ? a.t_y : a.y;
+            const int64_t e1 = rp[cur.r0 + 1];
+            double acc = 0.0;
+            for (int64_t q = cur.e0 + tid; q < e1; q += BLOCK) acc += vl[q] * wv(cl[q]);
+            const double dot = block_sum_n<BLOCK>(acc, red);
+            if (tid == 0) {
+                if (!cur.test) hinge += jmax(1 - yy[cur.r0] * dot, 0.0);
+                else err += (dot * yy[cur.r0] > 0) ? 0.0 : 1.0;
+            }
+            eval_fetch<BLOCK>(a, t + gridDim.x, ntiles, nxt);
+            cur = nxt;
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < R::RO; ++u) {
+            const int i = tid + u * BLOCK;
+            if (i <= cur.nr) roff[i] = cur.ro[u];
+        }
+#pragma unroll
+        for (int u = 0; u < R::PER; ++u) {
+            const int64_t i = tid + (int64_t)u * BLOCK;
+            if (i < cur.T) prod[i] = cur.v[u] * wv(cur.c[u]);
+        }
+        __syncthreads();
+        // next tile's HBM reads go out before the LDS row sums of this one
+        eval_fetch<BLOCK>(a, t + gridDim.x, ntiles, nxt);
+        const double* yy = cur.test ? a.t_y : a.y;
+        for (int r = grp; r < cur.nr; r += BLOCK / 16) {
+            const int32_t b = roff[r], e = roff[r + 1];
+            double acc = 0.0;
+            for (int32_t q = b + sub; q < e; q += 16) acc += prod[q];
+            const double dot = row16_sum(acc);
+            if (sub == 0) {
+                if (!cur.test) hinge += jmax(1 - yy[cur.r0 + r] * dot, 0.0);
+                else err += (dot * yy[cur.r0 + r] > 0) ? 0.0 : 1.0;
+            }
+        }
+        __syncthreads();
+        cur = nxt;
+    }
+    const int64_t gt = (int64_t)blockIdx.x * BLOCK + tid;
+    const int64_t gs = (int64_t)gridDim.x * BLOCK;
+    double al = 0.0, w2 = 0.0;
+    for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
+    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
+    const double s0 = block_sum_n<BLOCK>(hinge, red);
+    const double s1 = block_sum_n<BLOCK>(al, red);
+    const double s2 = block_sum_n<BLOCK>(w2, red);
+    const double s3 = block_sum_n<BLOCK>(err, red);
+    if (tid == 0) {
+        double* p = a.partials + (size_t)blockIdx.x * 4;
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+        p[3] = s3;
+    }
+}
+
 __global__ __launch_bounds__(256) void eval_final_kernel(const double* partials, int blocks, double* out) {
     __shared__ double red[4][4];
     const int tid = threadIdx.x;
@@ -144,6 +298,35 @@ int eval_fast_blocks(int64_t n_tiles, int64_t n_t_tiles) {
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
     eval_fast_kernel<<<blocks, kEvalBlock, 0, s>>>(a);
     eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+}
+
+int eval2_blocks(int version, int64_t n_tiles, int64_t n_t_tiles) {
+    int64_t b = n_tiles + n_t_tiles;
+    const int64_t cap = version == 2 ? 256 : 256 * kEval3BlocksPerCU;
+    if (b > cap) b = cap;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
+template <int BLOCK, bool WLDS>
+static void launch_pf(const EvalArgs& a, int blocks, hipStream_t s) {
+    const size_t lds = sizeof(double) * ((WLDS ? kEvalHotW : 0) + kEvalTile) + sizeof(int32_t) * (kEvalTile + 4) +
+                       sizeof(double) * (BLOCK / 64);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)eval_pf_kernel<BLOCK, WLDS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    eval_pf_kernel<BLOCK, WLDS><<<blocks, BLOCK, lds, s>>>(a);
+    eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+}
+
+void launch_eval2(int version, const EvalArgs& a, int blocks, hipStream_t s) {
+    if (version == 2)
+        launch_pf<1024, true>(a, blocks, s);
+    else
+        launch_pf<256, false>(a, blocks, s);
 }
 
 }  // namespace cocoa

@@ -76,6 +76,10 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
         mb->beg[lane] = beg;
         mb->y[lane] = yv;
         mb->q[lane] = qv;
+        if (!STRICT) {
+            const double qii = MODE == MODE_PLUS ? qv * a.sigma : qv;
+            mb->rq[lane] = qii != 0.0 ? 1.0 / qii : 0.0;
+        }
     }
     const int32_t T = __shfl(incl, m - 1, 64);
     // stream the batch's entries: 64 consecutive packed positions per unit
@@ -178,6 +182,7 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
     const int lane = lane_id();
     const int m = uni(mb->m);
     const double lam_n = a.lam_n;
+    const double inv_lam_n = 1.0 / a.lam_n;
     const double sigma = a.sigma;
 #ifdef COCOA_STEP_PROF
     uint64_t last_ = clock64();
@@ -259,8 +264,10 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
         if (fabs(proj) != 0.0) {                                 // CoCoA.scala:172
             const double qii = MODE == MODE_PLUS ? qv * sigma : qv;
             double na = 1.0;
-            if (qii != 0.0) na = jmin(jmax((aa - (grad / qii)), 0.0), 1.0);
-            const double coef = (yv * (na - aa)) / lam_n;        // CoCoA.scala:181
+            // fast mode multiplies by reciprocals staged off the chain (<= 1 ulp
+            // per operation; strict keeps the reference's two divisions)
+            if (qii != 0.0) na = jmin(jmax((aa - (STRICT ? grad / qii : grad * uni(mb->rq[s]))), 0.0), 1.0);
+            const double coef = STRICT ? (yv * (na - aa)) / lam_n : (yv * (na - aa)) * inv_lam_n;  // CoCoA.scala:181
             STEP_KEEP(coef);
             STEP_STAMP(3);
             if (fast_path) {
@@ -312,6 +319,143 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
     }
 }
 
+// ---------------------------------------------------------- chain v3 --
+// Fast-mode CoCoA+ / MbCD step chain.  Same staged batches as v1, but the
+// per-step work off the dependency chain is taken out of it:
+//   * the next step's metadata and (col, val) chunks are read from the LDS
+//     stream while the current step runs (they never change in a round);
+//   * the only dependent access per step is the gather of deltaW at the row's
+//     columns (LDS or the private HBM slice), issued for all chunks at once;
+//   * the update rule is branch-free: reciprocals staged by the loader replace
+//     the two divisions, fmin/fmax replace Java's Math.min/max (identical for
+//     the finite values reachable here; +-0 and NaN differ only in the sign of
+//     zero), and a skipped step (projected gradient 0) is coef = 0, na = aa.
+// Agrees with the strict path within the north_star tolerance (fast mode).
+struct Chunks3 {
+    int32_t c[kRegChunks];
+    double v[kRegChunks];
+};
+
+struct Meta3 {
+    int32_t r, off, z, fl;    // wave-uniform (SGPRs): control flow and addressing
+    double y, q, rq, xw, aa;  // broadcast LDS reads kept in VGPRs (no readfirstlane wait)
+};
+
+// Step metadata and alpha of the sampled row.  alpha is read before the
+// current step writes its own row; compute_batch3 forwards the new value when
+// the next step samples the same row.
+__device__ __forceinline__ Meta3 read_meta3(const BatchMeta* mb, int s, const double* alv) {
+    Meta3 m;
+    m.r = uni(mb->r[s]);
+    m.off = uni(mb->off[s]);
+    m.z = uni(mb->z[s]);
+    m.fl = uni(mb->flags[s]);
+    m.y = mb->y[s];
+    m.q = mb->q[s];
+    m.rq = mb->rq[s];
+    m.xw = mb->xw[s];
+    m.aa = alv[m.r];
+    return m;
+}
+
+// (col, val) of a staged row, branch-free: lanes past z read the row's last
+// entry (a valid column) with value 0.
+__device__ __forceinline__ void read_chunks3(const int32_t* scol, const double* sval, const Meta3& m, Chunks3& ch) {
+    const int lane = lane_id();
+    const bool ok = m.off >= 0 && m.z > 0;
+    const int32_t last = ok ? m.off + m.z - 1 : 0;
+#pragma unroll
+    for (int u = 0; u < kRegChunks; ++u) {
+        const int32_t p = lane + 64 * u;
+        const int32_t q = min(m.off + p, last);
+        ch.c[u] = scol[q];
+        const double v = sval[q];
+        ch.v[u] = (ok && p < m.z) ? v : 0.0;
+    }
+}
+
+template <int MODE, bool VEC_LDS>
+__device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const int32_t* scol, const double* sval,
+                               double* vec, double* alv) {
+    const int lane = lane_id();
+    const int m = uni(mb->m);
+    const double lam_n = a.lam_n;
+    const double inv_lam_n = 1.0 / a.lam_n;
+    const double sigma = a.sigma;
+    Meta3 nm = read_meta3(mb, 0, alv);
+    Chunks3 nc;
+    read_chunks3(scol, sval, nm, nc);
+    for (int s = 0; s < m; ++s) {
+        const Meta3 st = nm;
+        const Chunks3 ch = nc;
+        const int nch = (st.z + 63) >> 6;
+        const bool regs = st.off >= 0 && nch <= kRegChunks && (st.fl & 1) == 0;
+        // 1. the dependent gather of this step goes out first ...
+        double pd[kRegChunks];
+        if (MODE == MODE_PLUS && regs) {
+#pragma unroll
+            for (int u = 0; u < kRegChunks; ++u) pd[u] = u < nch ? vec[ch.c[u]] : 0.0;
+        }
+        // 2. ... then the next step's staged inputs (independent of the chain)
+        if (s + 1 < m) {
+            nm = read_meta3(mb, s + 1, alv);
+            read_chunks3(scol, sval, nm, nc);
+        }
+        const double aa = st.aa;
+        double sdot = 0.0;
+        if (MODE == MODE_PLUS) {
+            if (regs) {
+                double acc = 0.0;
+#pragma unroll
+                for (int u = 0; u < kRegChunks; ++u) acc = fma(ch.v[u], pd[u], acc);
+                sdot = wave_sum(acc);
+            } else {
+                const int32_t* sc = st.off >= 0 ? scol + st.off : a.col + uni(mb->beg[s]);
+                const double* sv = st.off >= 0 ? sval + st.off : a.val + uni(mb->beg[s]);
+                double acc = 0.0;
+                for (int32_t p = lane; p < st.z; p += 64) acc += sv[p] * vec[sc[p]];
+                sdot = wave_sum(acc);
+            }
+        }
+        // CoCoA.scala:159-186 / MinibatchCD.scala:104-123, branch-free
+        const double grad = MODE == MODE_PLUS ? (st.y * (st.xw + sigma * sdot) - 1.0) * lam_n
+                                              : (st.y * st.xw - 1.0) * lam_n;
+        const double proj = aa <= 0.0 ? fmin(grad, 0.0) : (aa >= 1.0 ? fmax(grad, 0.0) : grad);
+        const bool go = proj != 0.0;
+        const double qii = MODE == MODE_PLUS ? st.q * sigma : st.q;
+        const double nt = fmin(fmax(aa - grad * st.rq, 0.0), 1.0);
+        const double na = go ? (qii != 0.0 ? nt : 1.0) : aa;
+        const double coef = (st.y * (na - aa)) * inv_lam_n;
+        if (s + 1 < m && nm.r == st.r) nm.aa = na;               // same row sampled twice in a row
+        if (uni((int32_t)go)) {
+            if (regs) {
+#pragma unroll
+                for (int u = 0; u < kRegChunks; ++u) {
+                    if (u < nch && lane + 64 * u < st.z) {
+                        if (MODE == MODE_PLUS) {
+                            vec[ch.c[u]] = fma(ch.v[u], coef, pd[u]);  // deltaW += update
+                        } else if (VEC_LDS) {
+                            atomicAdd(vec + ch.c[u], ch.v[u] * coef);
+                        } else {
+                            unsafeAtomicAdd(vec + ch.c[u], ch.v[u] * coef);
+                        }
+                    }
+                }
+            } else {
+                const int32_t* sc = st.off >= 0 ? scol + st.off : a.col + uni(mb->beg[s]);
+                const double* sv = st.off >= 0 ? sval + st.off : a.val + uni(mb->beg[s]);
+                if (st.fl & 1) {
+                    if (lane == 0)
+                        for (int32_t q = 0; q < st.z; ++q) vec[sc[q]] = vec[sc[q]] + sv[q] * coef;
+                } else {
+                    for (int32_t p = lane; p < st.z; p += 64) vec[sc[p]] = vec[sc[p]] + sv[p] * coef;
+                }
+            }
+            if (lane == 0) alv[st.r] = na;                       // CoCoA.scala:186
+        }
+    }
+}
+
 template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS>
 __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -354,6 +498,9 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
             load_batch<MODE, STRICT>(a, k, p0, cursor, (BatchMeta*)(lds + a.lds_meta[cur ^ 1]),
                                      (int32_t*)(lds + a.lds_stream_col[cur ^ 1]), (double*)(lds + a.lds_stream_val[cur ^ 1]),
                                      prod);
+        } else if (!STRICT && MODE != MODE_COCOA && a.chain == 3) {
+            compute_batch3<MODE, VEC_LDS>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
+                                          (const double*)(lds + a.lds_stream_val[cur]), vec, alv);
         } else {
             compute_batch<MODE, STRICT, VEC_LDS, ALPHA_LDS>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
                                                             (const double*)(lds + a.lds_stream_val[cur]), scratch, vec,

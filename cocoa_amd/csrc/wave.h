@@ -35,12 +35,22 @@ __device__ __forceinline__ double dpp_d(double x) {
     return __longlong_as_double((int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
 }
 
+// In-row DPP move with every source lane valid (quad_perm / row_ror): no
+// "old" operand, so no zero-initialising moves are emitted.
+template <int CTRL>
+__device__ __forceinline__ double dpp_row_d(double x) {
+    const int64_t b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)((uint64_t)b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double((int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
 // Sum within each DPP row of 16 lanes; every lane of the row ends with the sum.
 __device__ __forceinline__ double row16_sum(double x) {
-    x += dpp_d<0xB1>(x);   // quad_perm [1,0,3,2]
-    x += dpp_d<0x4E>(x);   // quad_perm [2,3,0,1]
-    x += dpp_d<0x124>(x);  // row_ror:4
-    x += dpp_d<0x128>(x);  // row_ror:8
+    x += dpp_row_d<0xB1>(x);   // quad_perm [1,0,3,2]
+    x += dpp_row_d<0x4E>(x);   // quad_perm [2,3,0,1]
+    x += dpp_row_d<0x124>(x);  // row_ror:4
+    x += dpp_row_d<0x128>(x);  // row_ror:8
     return x;
 }
 
