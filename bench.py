@@ -170,8 +170,8 @@ def main():
     # profiled the same kernel variant this run launched
     plan = eng.plan()
     solver_tag = "solver2_kernel" if plan.get("solver") == "v2" else "solver_kernel<"
-    eval_tag = {"v1": "eval_fast_kernel", "v2": "eval_pf_kernel<1024", "v3": "eval_pf_kernel<256"}[
-        os.environ.get("COCOA_EVAL", "v1") if os.environ.get("COCOA_EVAL", "v1") in ("v1", "v2", "v3") else "v1"]
+    eval_tag = {"v1": "eval_fast_kernel", "v2": "eval_pf_kernel<1024", "v3": "eval_pf_kernel<256",
+                "v4": "eval_v4_kernel<4096, 512, 1"}.get(os.environ.get("COCOA_EVAL", "v4"), "eval_v4_kernel<4096, 512, 1")
     traffic = traffic_eval = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf) and not args.strict:

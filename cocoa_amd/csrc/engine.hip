@@ -99,8 +99,8 @@ struct cocoa_ctx {
     Csr te;
     bool has_test = false;
     // row tiles of the fast evaluation pass
-    DevBuf tiles, t_tiles;
-    int64_t n_tiles = 0, n_t_tiles = 0;
+    DevBuf tiles, t_tiles, tiles4k, t_tiles4k;  // kEvalTile and 4096-entry tiles (eval v4)
+    int64_t n_tiles = 0, n_t_tiles = 0, n_tiles4k = 0, n_t_tiles4k = 0;
     // device feature order (see cocoa_set_train)
     std::vector<int32_t> perm, inv;
     std::vector<int64_t> n_hot_nnz;
@@ -287,17 +287,26 @@ static void upload(DevBuf& b, const void* src, size_t bytes, hipStream_t s) {
     if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s));
 }
 
+// CSR entry arrays get 64 zero bytes of tail padding: the 16-byte loads of
+// eval v4 read whole 4-entry units from an aligned base, so the last unit of
+// the last tile may extend up to 3 entries past nnz.
+static void upload_padded(DevBuf& b, const void* src, size_t bytes, hipStream_t s) {
+    b.alloc(bytes + 64);
+    HIPCHK(hipMemsetAsync((char*)b.p + bytes, 0, 64, s));
+    if (bytes) HIPCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, s));
+}
+
 // Row tiles for the fast eval pass: whole rows, <= kEvalTile entries and rows
 // per tile; a row longer than kEvalTile is a tile of its own.
-static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStream_t s) {
+static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStream_t s, int64_t cap = kEvalTile) {
     std::vector<int64_t> t{0};
     int64_t r = 0;
     while (r < n) {
         const int64_t start = r, e0 = row_ptr[r];
-        if (row_ptr[r + 1] - e0 > kEvalTile) {
+        if (row_ptr[r + 1] - e0 > cap) {
             ++r;
         } else {
-            while (r < n && row_ptr[r + 1] - e0 <= kEvalTile && r - start < kEvalTile) ++r;
+            while (r < n && row_ptr[r + 1] - e0 <= cap && r - start < cap) ++r;
         }
         t.push_back(r);
     }
@@ -398,13 +407,14 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     upload(ctx->d_perm, ctx->perm.data(), sizeof(int32_t) * (size_t)num_features, s);
     upload(ctx->d_inv, ctx->inv.data(), sizeof(int32_t) * (size_t)num_features, s);
     upload(ctx->tr.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
-    upload(ctx->tr.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
-    upload(ctx->tr.val, val, sizeof(double) * (size_t)nnz, s);
+    upload_padded(ctx->tr.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
+    upload_padded(ctx->tr.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s);
+    ctx->n_tiles4k = make_tiles(row_ptr, n_rows, ctx->tiles4k, s, 4096);
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
     CAPI_END(ctx)
@@ -423,10 +433,11 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
     std::vector<int32_t> pcol((size_t)std::max<int64_t>(nnz, 1));
     for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];  // device feature order
     upload(ctx->te.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
-    upload(ctx->te.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
-    upload(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
+    upload_padded(ctx->te.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
+    upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s);
+    ctx->n_t_tiles4k = make_tiles(row_ptr, n_rows, ctx->t_tiles4k, s, 4096);
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     if (ctx->inited) {
@@ -554,14 +565,18 @@ static void plan_solver2(cocoa_ctx* c, int32_t max_nl) {
     c->lds2_bytes = off;
 }
 
-// fast eval kernel: COCOA_EVAL=v1 (tile stream; default), v2 (hot w in LDS +
-// tile prefetch, one block per CU), v3 (tile prefetch, 6 blocks per CU).
-// Measured on C2 (r01): v1 0.238 ms, v2 0.320 ms, v3 0.274 ms.
+// fast eval kernel: COCOA_EVAL=v4 (default: 16-byte tile stream, variant
+// COCOA_EVAL4, default 3 = 4096-entry tiles, 512 threads, 3 blocks per CU),
+// v1 (4/8-byte tile stream), v2 (hot w in LDS + tile prefetch, one block per
+// CU), v3 (tile prefetch, 6 blocks per CU).  Measured on C2 (r01): v4 0.212 ms,
+// v1 0.236 ms, v2 0.320 ms, v3 0.274 ms; v4 without the w gather (diagnostic
+// variant 2) 0.104 ms, so the gather of w costs ~45% of the pass.
 static int eval_version() {
     const char* e = std::getenv("COCOA_EVAL");
+    if (e && std::strcmp(e, "v1") == 0) return 1;
     if (e && std::strcmp(e, "v2") == 0) return 2;
     if (e && std::strcmp(e, "v3") == 0) return 3;
-    return 1;
+    return 4;
 }
 
 // v2 is opt-in (COCOA_SOLVER=v2): on C2 it measured 10.5 ms/round against
@@ -852,6 +867,17 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
             launch_eval_strict(e, ctx->stream);
         else if (eval_version() == 1)
             launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
+        else if (eval_version() == 4) {
+            const char* ev = std::getenv("COCOA_EVAL4");
+            const int var = ev ? std::atoi(ev) : 3;
+            if (eval4_tile(var) == 4096) {  // v4 variant tiles
+                e.tiles = ctx->tiles4k.as<int64_t>();
+                e.n_tiles = ctx->n_tiles4k;
+                e.t_tiles = ctx->has_test ? ctx->t_tiles4k.as<int64_t>() : nullptr;
+                e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles4k : 0;
+            }
+            launch_eval4(var, e, eval4_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
+        }
         else
             launch_eval2(eval_version(), e, eval2_blocks(eval_version(), e.n_tiles, e.n_t_tiles), ctx->stream);
     });

@@ -330,3 +330,164 @@ void launch_eval2(int version, const EvalArgs& a, int blocks, hipStream_t s) {
 }
 
 }  // namespace cocoa
+
+namespace cocoa {
+
+// Eval v4: the v1 tile stream with 16-byte loads.  A tile [e0, e1) is read from
+// the 4-entry-aligned base e0 & ~3, so each thread moves 4 consecutive entries
+// per unit with one 16-B col load and two 16-B val loads (v1 moves 4 B + 8 B
+// per lane).  Row offsets inside a tile are 16-bit (a tile holds <= TILE <=
+// 65536 entries), which leaves room for more blocks per CU.
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// GATHER: 1 = w gathered from global (the product); diagnostics (wrong values,
+// timing only): 0 = no gather, 2 = 1 lane in 8 gathers, 3 = gathered from a
+// 2048-double LDS copy of the head of w.
+template <int TILE, int BLOCK, int GATHER>
+__global__ __launch_bounds__(BLOCK) void eval_v4_kernel(EvalArgs a) {
+    constexpr int UNITS = TILE / (4 * BLOCK);  // 4-entry units per thread (base alignment adds one)
+    __shared__ double prod[TILE + 4];
+    __shared__ double wl[GATHER == 3 ? 2048 : 1];
+    if (GATHER == 3) {
+        for (int j = threadIdx.x; j < 2048; j += BLOCK) wl[j] = j < a.d ? a.w[j] : 0.0;
+        __syncthreads();
+    }
+    auto wg = [&](double v, int32_t c) -> double {
+        if (GATHER == 1) return v * a.w[c];
+        if (GATHER == 2) return (c & 7) == 0 ? v * a.w[c] : v;
+        if (GATHER == 3) return v * wl[c & 2047];
+        if (GATHER == 5) return v * a.w[c & 2047];
+        return v;
+    };
+    __shared__ uint16_t roff[TILE + 2];
+    __shared__ double red[BLOCK / 64];
+    const int tid = threadIdx.x;
+    const int sub = tid & 15, grp = tid >> 4;
+    double hinge = 0.0, err = 0.0;
+    const int64_t ntiles = a.n_tiles + a.n_t_tiles;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const bool test = t >= a.n_tiles;
+        const int64_t tt = test ? t - a.n_tiles : t;
+        const int64_t* tl = test ? a.t_tiles : a.tiles;
+        const int64_t* te = tl + (test ? a.n_t_tiles : a.n_tiles) + 1;
+        const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
+        const int32_t* cl = test ? a.t_col : a.col;
+        const double* vl = test ? a.t_val : a.val;
+        const double* yy = test ? a.t_y : a.y;
+        const int64_t r0 = tl[tt], r1 = tl[tt + 1];
+        const int64_t e0 = te[tt], e1 = te[tt + 1];
+        const int64_t T = e1 - e0;
+        if (T > TILE) {
+            double acc = 0.0;
+            for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += wg(vl[q], cl[q]);
+            const double dot = block_sum_n<BLOCK>(acc, red);
+            if (tid == 0) {
+                if (!test) hinge += jmax(1 - yy[r0] * dot, 0.0);
+                else err += (dot * yy[r0] > 0) ? 0.0 : 1.0;
+            }
+            continue;
+        }
+        const int nr = (int)(r1 - r0);
+        for (int i = tid; i <= nr; i += BLOCK) roff[i] = (uint16_t)(rp[r0 + i] - e0);
+        const int64_t base = e0 & ~(int64_t)3;
+        const int sh = (int)(e0 - base);  // prod[k] holds entry base + k; rows index from sh
+        const int64_t span = e1 - base;
+        i32x4 c[UNITS + 1];
+        f64x2 v0[UNITS + 1], v1[UNITS + 1];
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            c[u] = i32x4{0, 0, 0, 0};
+            v0[u] = f64x2{0.0, 0.0};
+            v1[u] = v0[u];
+            if (k < span) {
+                c[u] = __builtin_nontemporal_load((const i32x4*)(cl + base + k));
+                v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
+                v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            if (k < span) {
+                // entries past e1 inside the last unit are never summed (roff bounds rows)
+                const double p0 = wg(v0[u].x, c[u].x);
+                const double p1 = wg(v0[u].y, c[u].y);
+                const double p2 = wg(v1[u].x, c[u].z);
+                const double p3 = wg(v1[u].y, c[u].w);
+                *(f64x2*)(prod + k) = f64x2{p0, p1};
+                *(f64x2*)(prod + k + 2) = f64x2{p2, p3};
+            }
+        }
+        __syncthreads();
+        for (int r = grp; r < nr; r += BLOCK / 16) {
+            const int b = roff[r] + sh, e = roff[r + 1] + sh;
+            double acc = 0.0;
+            for (int q = b + sub; q < e; q += 16) acc += prod[q];
+            const double dot = row16_sum(acc);
+            if (sub == 0) {
+                if (!test) hinge += jmax(1 - yy[r0 + r] * dot, 0.0);
+                else err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t gt = (int64_t)blockIdx.x * BLOCK + tid;
+    const int64_t gs = (int64_t)gridDim.x * BLOCK;
+    double al = 0.0, w2 = 0.0;
+    for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
+    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
+    const double s0 = block_sum_n<BLOCK>(hinge, red);
+    const double s1 = block_sum_n<BLOCK>(al, red);
+    const double s2 = block_sum_n<BLOCK>(w2, red);
+    const double s3 = block_sum_n<BLOCK>(err, red);
+    if (tid == 0) {
+        double* p = a.partials + (size_t)blockIdx.x * 4;
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+        p[3] = s3;
+    }
+}
+
+int eval4_tile(int variant) { return variant == 1 || variant == 3 || variant >= 4 ? 4096 : 2048; }
+
+// variant: 0 = tile 2048 / 8 blocks per CU, 1 = tile 4096 / 4 per CU,
+//          2 = tile 2048 without the w gather (diagnostic: stream-only time),
+//          3 = tile 4096 / 4 per CU, 512 threads
+int eval4_blocks(int variant, int64_t n_tiles, int64_t n_t_tiles) {
+    const int per_cu = variant >= 8 ? 2 : (variant == 1 || variant >= 3 ? 3 : 7);  // LDS: 41 KB / 20.5 KB per block
+    int64_t b = n_tiles + n_t_tiles;
+    if (b > 256 * per_cu) b = 256 * per_cu;
+    return (int)(b < 1 ? 1 : b);
+}
+
+void launch_eval4(int variant, const EvalArgs& a, int blocks, hipStream_t s) {
+    if (variant == 1)
+        eval_v4_kernel<4096, 256, 1><<<blocks, 256, 0, s>>>(a);
+    else if (variant == 2)
+        eval_v4_kernel<2048, 256, 0><<<blocks, 256, 0, s>>>(a);
+    else if (variant == 3)
+        eval_v4_kernel<4096, 512, 1><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 4)
+        eval_v4_kernel<4096, 512, 2><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 5)
+        eval_v4_kernel<4096, 512, 3><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 6)
+        eval_v4_kernel<4096, 512, 0><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 7)
+        eval_v4_kernel<4096, 512, 5><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 8)
+        eval_v4_kernel<4096, 1024, 1><<<blocks, 1024, 0, s>>>(a);
+    else if (variant == 9)
+        eval_v4_kernel<4096, 1024, 5><<<blocks, 1024, 0, s>>>(a);
+    else if (variant == 10)
+        eval_v4_kernel<4096, 1024, 0><<<blocks, 1024, 0, s>>>(a);
+    else
+        eval_v4_kernel<2048, 256, 1><<<blocks, 256, 0, s>>>(a);
+    eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+}
+
+}  // namespace cocoa
+

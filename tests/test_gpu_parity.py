@@ -287,3 +287,50 @@ def test_c2_fast_properties(c2):
     assert gaps[-1] < gaps[0]
     es = s.eval()
     assert abs(es["primal"] - f.eval()["primal"]) <= REL * es["primal"]
+
+
+def _eval_edge_data(seed=11):
+    """Rows longer than both eval tile sizes (2048 / 4096 entries), empty rows
+    and ragged lengths, so tiles start at every alignment mod 4."""
+    rng = np.random.default_rng(seed)
+    d = 9000
+    rows = []
+    for r in range(1500):
+        if r % 89 == 4:
+            z = 0
+        elif r % 211 == 17:
+            z = 5000
+        elif r % 113 == 50:
+            z = 3000
+        else:
+            z = int(rng.integers(1, 120))
+        cols = np.sort(rng.choice(d, size=z, replace=False)).astype(np.int32)
+        vals = rng.standard_normal(z)
+        rows.append((cols, vals / max(np.linalg.norm(vals), 1e-300)))
+    row_ptr = np.concatenate([[0], np.cumsum([len(c) for c, _ in rows])]).astype(np.int64)
+    y = np.where(rng.random(1500) < 0.5, 1.0, -1.0)
+    part = np.array([0, 400, 800, 1100, 1500], np.int64)
+    return LabeledData(row_ptr, np.concatenate([c for c, _ in rows]).astype(np.int32),
+                       np.concatenate([v for _, v in rows]), y, part, d)
+
+
+@pytest.mark.parametrize("version,variant", [("v1", "3"), ("v4", "0"), ("v4", "1"), ("v4", "3")])
+def test_fast_eval_versions_match_oracle(version, variant, monkeypatch):
+    """Every fast eval kernel (OptUtils.scala:57-98) against the oracle on the
+    same (w, alpha), including rows longer than a tile and empty rows."""
+    monkeypatch.setenv("COCOA_EVAL", version)
+    monkeypatch.setenv("COCOA_EVAL4", variant)
+    tr = _eval_edge_data()
+    te = tr.row_range(200, 1300)
+    od, ot = odata(tr), odata(te)
+    run = oracle.Run(od, "cocoa+", tr.n, 200, 2e-3, seed=3)
+    for t in range(1, 4):
+        run.round(t)
+    e = engine(tr, te, strict=False)
+    e.init("cocoa+", tr.n, 0, 200, 2e-3)
+    e.set_w(run.w())
+    e.set_alpha(run.alpha())
+    ev, rv = e.eval(), run.eval(ot)
+    for k in ("primal", "dual", "gap"):
+        assert abs(ev[k] - rv[k]) <= 1e-12 * abs(rv["primal"]), k
+    assert ev["test_err_count"] == rv["test_err"]
