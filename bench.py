@@ -29,6 +29,22 @@ METRIC = "CoCoA+ SVM wall-clock to duality gap 1e-4; coord updates/s at 1/2/4/8 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
 
 
+# BASELINE.json configs.  c2 is the headline line the
+# driver runs; c3 (epsilon-shaped dense) and c4 (url-shaped, K=1024) are extra
+# measurement lines, c5 is c2 with --method over the five methods.
+_SYN = "synthetic: seeded {} generator ({}); no dataset download"
+CONFIGS = {
+    "c2": dict(kind="rcv1", n=677399, d=47236, nnz=75.6, parts=64, lam=1e-4, n_test=50000, shape="rcv1-shaped",
+               data=_SYN.format("rcv1-shaped", "Zipf columns, unit-norm tf-idf-like rows, planted separator + 10% noise")),
+    "c3": dict(kind="epsilon", n=400000, d=2000, nnz=2000.0, parts=64, lam=1e-4, n_test=10000,
+               shape="epsilon-shaped dense",
+               data=_SYN.format("epsilon-shaped", "dense N(0,1) rows, L2-normalised, planted separator")),
+    "c4": dict(kind="url", n=2396130, d=3231961, nnz=116.0, parts=1024, lam=1e-4, n_test=20000,
+               shape="url-shaped very sparse",
+               data=_SYN.format("url-shaped", "heavy-Zipf columns, ~116 nnz/row, planted separator")),
+}
+
+
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
@@ -54,21 +70,32 @@ def solver_bytes_per_round(tr, H, seed_t, plus=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="BASELINE.json config (c2 = the headline line; c3/c4 are extra measurement lines)")
+    ap.add_argument("--method", default="cocoa+", choices=["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"],
+                    help="C5 five-method comparison: the method whose rounds are timed")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--strict", action="store_true", help="bit-exact mode (default: fast)")
-    ap.add_argument("--n", type=int, default=677399)
-    ap.add_argument("--d", type=int, default=47236)
-    ap.add_argument("--nnz", type=float, default=75.6)
-    ap.add_argument("--parts", type=int, default=64)
-    ap.add_argument("--lam", type=float, default=1e-4)
-    ap.add_argument("--n-test", type=int, default=50000)
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--d", type=int, default=None)
+    ap.add_argument("--nnz", type=float, default=None)
+    ap.add_argument("--parts", type=int, default=None)
+    ap.add_argument("--lam", type=float, default=None)
+    ap.add_argument("--n-test", type=int, default=None)
     ap.add_argument("--gap-target", type=float, default=1e-4)
     ap.add_argument("--gap-max-rounds", type=int, default=400)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gap", action="store_true")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    for k in ("n", "d", "nnz", "parts", "lam", "n_test"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfg[k])
+    sdca = args.method in ("cocoa+", "cocoa", "mbcd")  # methods with a dual (alpha) and so a duality gap
+    if not sdca:
+        args.no_gap = True
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -86,7 +113,7 @@ def main():
     t0 = time.time()
     rows = args.n + args.n_test
     stride = ((rows + 4095) // 4096) * 4096
-    allr = cocoa_amd.gen_synthetic("rcv1", rows, args.d, args.nnz, 1, 12345, first_row=rank * stride,
+    allr = cocoa_amd.gen_synthetic(cfg["kind"], rows, args.d, args.nnz, 1, 12345, first_row=rank * stride,
                                    threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     tr = allr.row_range(0, args.n)
     tr.part_ptr = balanced(args.n, args.parts)
@@ -100,7 +127,7 @@ def main():
     eng = TorchEngine(device=local_rank, strict=args.strict)
     eng.set_train(tr, part_begin=rank * args.parts, num_parts_global=K_glob)
     eng.set_test(te)
-    eng.init("cocoa+", n_glob, 1 << 30, H, args.lam)
+    eng.init(args.method, n_glob, 1 << 30, H, args.lam)
     runner = DistributedCoCoA(eng)
 
     def barrier():
@@ -131,7 +158,7 @@ def main():
     for _ in range(args.steps):
         runner.round(t)
         ev = runner.eval()
-        gaps.append(ev["gap"])
+        gaps.append(ev["gap"] if sdca else ev["primal"])
         timed_rounds.append(t)
         t += 1
     barrier()
@@ -147,7 +174,7 @@ def main():
     rounds_to_gap = None
     final_gap = None
     if not args.no_gap:
-        eng.init("cocoa+", n_glob, 1 << 30, H, args.lam)
+        eng.init(args.method, n_glob, 1 << 30, H, args.lam)
         barrier()
         tg = time.perf_counter()
         for r in range(1, args.gap_max_rounds + 1):
@@ -163,7 +190,8 @@ def main():
 
     # ---- roofline of the dominant kernel (solver) and of the eval pass -----
     solver_ms = stats["solver"]["total_ms"] / max(stats["solver"]["launches"], 1)
-    b_solver = np.mean([solver_bytes_per_round(tr, H, t_ + 0) for t_ in timed_rounds[:4]])
+    b_solver = np.mean([solver_bytes_per_round(tr, H, t_ + 0, plus=args.method != "cocoa")
+                        for t_ in timed_rounds[:4]])
     ach = b_solver / (solver_ms * 1e-3) / 1e9
     # HBM traffic per launch from the committed PMC passes (tools/gpu_pmc.sh ->
     # tools/pmc_summary.py -> profiles/traffic.json), used only when the PMC run
@@ -195,7 +223,7 @@ def main():
         from oracle import oracle
         cores = min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
         od = oracle.Data(tr.row_ptr, tr.col, tr.val, tr.y, tr.part_ptr, tr.num_features)
-        run = oracle.Run(od, "cocoa+", tr.n, H, args.lam, nthreads=cores)
+        run = oracle.Run(od, args.method, tr.n, H, args.lam, nthreads=cores)
         tc = time.perf_counter()
         run.round(1)
         t1 = time.perf_counter() - tc
@@ -205,7 +233,7 @@ def main():
             run.round(r)
         tcpu = time.perf_counter() - tc
         cpu = {"value": args.parts * H * R / tcpu, "unit": "coord updates/s", "cores": cores, "kind": "port",
-               "sample": f"{R} CoCoA+ rounds of the same C2 shard (K={args.parts}, H={H}) by the strict C oracle "
+               "sample": f"{R} {args.method} rounds of the same {args.config.upper()} shard (K={args.parts}, H={H}) by the strict C oracle "
                          f"(oracle/cocoa_oracle.c), one pthread per partition group, {tcpu:.1f}s"}
         log(f"cpu baseline {cpu}")
 
@@ -214,13 +242,14 @@ def main():
             "metric": METRIC, "value": value, "unit": "coord updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: seeded rcv1-shaped generator (Zipf columns, unit-norm tf-idf-like rows, planted "
-                    "separator + 10% noise); no dataset download",
-            "config": {"workload": "C2 rcv1-shaped CoCoA+ (n=677399/GPU, d=47236, ~75.6 nnz/row, lambda=1e-4, "
-                                   "K=64/GPU, H=n/K=10584), step = round + gap eval",
+            "data": cfg["data"],
+            "config": {"workload": f"{args.config.upper()} {cfg['shape']} {args.method} (n={args.n}/GPU, d={args.d}, "
+                                   f"~{args.nnz} nnz/row, lambda={args.lam}, K={args.parts}/GPU, H=n/K={H}), "
+                                   f"step = round + {'gap' if sdca else 'primal'} eval",
+                       "method": args.method,
                        "n_total": n_glob, "K_total": K_glob, "H": H, "nnz_per_gpu": tr.nnz, "test_rows_per_gpu": te.n,
                        "mode": "strict" if args.strict else "fast",
-                       "parallelism": f"dp{world}: 64 partitions per GPU, deltaW all-reduce (RCCL)"},
+                       "parallelism": f"dp{world}: {args.parts} partitions per GPU, deltaW all-reduce (RCCL)"},
             "time_to_gap_s": ttg, "rounds_to_gap": rounds_to_gap, "gap_target": args.gap_target,
             "final_gap": final_gap, "gap_trajectory_timed": gaps,
             "roofline": {"kernel": "solver (local SDCA, CoCoA.localSDCA)", "bound": "hbm", "achieved": ach,

@@ -768,7 +768,12 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
                 c->mult = step * c->scaling;                                 // SGD.scala:58
             }
             const double t0 = (double)wrap32((int64_t)(t - 1) * H * c->K_glob); // SGD.scala:53 (Int)
-            c->timed(COCOA_K_SOLVER, [&] { launch_sgd(local, c->sa, c->P.lambda, t0, K, s); });
+            c->timed(COCOA_K_SOLVER, [&] {
+                if (c->strict)
+                    launch_sgd(local, c->sa, c->P.lambda, t0, K, s);
+                else
+                    launch_sgd_fast(local, c->sa, c->P.lambda, t0, K, s);
+            });
         }
     } else if (c->method == COCOA_METHOD_MBSGD) {
         const double step = 1 / (c->P.lambda * (double)t);

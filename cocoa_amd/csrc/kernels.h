@@ -204,5 +204,6 @@ void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const
 void launch_scale(double* w, int64_t d, double scale, hipStream_t s);
 void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, double* out, hipStream_t s);
 void launch_sgd(bool local, const SolverArgs& a, double lambda, double t0, int grid, hipStream_t s);
+void launch_sgd_fast(bool local, const SolverArgs& a, double lambda, double t0, int K, hipStream_t s);
 
 }  // namespace cocoa

@@ -491,3 +491,95 @@ void launch_eval4(int variant, const EvalArgs& a, int blocks, hipStream_t s) {
 
 }  // namespace cocoa
 
+
+namespace cocoa {
+
+// ------------------------------------------------------- fast SGD (C5) --
+// mb-SGD (SGD.scala:87-139 with local = false): within a round every sampled
+// row is tested against the same driver w, so the H steps of a partition are
+// independent.  One wave per coordinate step over all K_loc * H steps of the
+// launch: wave-tree x.w, and a violator (1 - y x.w > 0, SGD.scala:115,124)
+// adds x*y into its partition's private deltaW slice with fire-and-forget
+// atomics (sum order differs from the reference's sequential adds: fast mode).
+__global__ __launch_bounds__(256) void mbsgd_fast_kernel(SolverArgs a, int32_t K) {
+    const int lane = threadIdx.x & 63;
+    const int64_t total = (int64_t)K * a.H;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < total; g += nw) {
+        const int32_t k = (int32_t)(g / a.H);
+        const int64_t gr = a.part_ptr[k] + a.samples[g];
+        const int64_t b = a.row_ptr[gr], e = a.row_ptr[gr + 1];
+        const double yv = a.y[gr];
+        double acc = 0.0;
+        for (int64_t q = b + lane; q < e; q += 64) acc = fma(a.val[q], a.w[a.col[q]], acc);
+        const double dot = wave_sum(acc);
+        if (1.0 - yv * dot > 0) {
+            double* dwk = a.dw + (size_t)k * a.d;
+            for (int64_t q = b + lane; q < e; q += 64) unsafeAtomicAdd(dwk + a.col[q], a.val[q] * yv);
+        }
+    }
+}
+
+// local SGD (SGD.scala:87-139 with local = true): one wave per partition runs
+// the sequential chain.  The reference shrinks its whole w copy by
+// (1 - step*lambda) every step (O(d), SGD.scala:119-120); here w = s * v with
+// the shrink folded into the scalar s, so a step costs O(z):
+//   x.w = s (x.v);  s *= 1 - step*lambda;  v += x*y*step / s  (if violator).
+// A shrink factor of exactly 0 (the first step of round 1) zeroes v and
+// resets s; a tiny s is folded back into v.  deltaW = s v - wInit.
+__device__ void localsgd_rescale(double* v, int64_t d, double f) {
+    for (int64_t j = lane_id(); j < d; j += 64) v[j] = v[j] * f;
+}
+
+__global__ __launch_bounds__(64) void localsgd_fast_kernel(SolverArgs a, double lambda, double t0) {
+    const int k = blockIdx.x;
+    const int lane = lane_id();
+    const int64_t p0 = a.part_ptr[k];
+    const int64_t d = a.d;
+    double* v = a.wloc + (size_t)k * d;
+    double* dwk = a.dw + (size_t)k * d;
+    for (int64_t j = lane; j < d; j += 64) v[j] = a.w[j];
+    double s = 1.0;
+    for (int32_t i = 1; i <= a.H; ++i) {
+        const double step = 1.0 / (lambda * (t0 + (double)i));          // SGD.scala:106
+        const int64_t gr = p0 + a.samples[(size_t)k * a.H + (i - 1)];
+        const int64_t b = a.row_ptr[gr], e = a.row_ptr[gr + 1];
+        const double yv = a.y[gr];
+        double acc = 0.0;
+        for (int64_t q = b + lane; q < e; q += 64) acc = fma(a.val[q], v[a.col[q]], acc);
+        const double ev = 1.0 - yv * (s * wave_sum(acc));                // SGD.scala:115
+        const double scale = 1.0 - step * lambda;                        // SGD.scala:119-120
+        if (scale == 0.0) {
+            localsgd_rescale(v, d, 0.0);
+            s = 1.0;
+        } else {
+            s *= scale;
+        }
+        if (ev > 0) {                                                    // SGD.scala:124-130
+            const double u = (yv * step) / s;
+            if (a.any_dup && a.rowflags && (a.rowflags[gr] & 1)) {
+                if (lane == 0)
+                    for (int64_t q = b; q < e; ++q) v[a.col[q]] = v[a.col[q]] + a.val[q] * u;
+            } else {
+                for (int64_t q = b + lane; q < e; q += 64) v[a.col[q]] = fma(a.val[q], u, v[a.col[q]]);
+            }
+        }
+        if (fabs(s) < 1e-150) {
+            localsgd_rescale(v, d, s);
+            s = 1.0;
+        }
+    }
+    for (int64_t j = lane; j < d; j += 64) dwk[j] = s * v[j] - a.w[j];  // SGD.scala:133
+}
+
+void launch_sgd_fast(bool local, const SolverArgs& a, double lambda, double t0, int K, hipStream_t s) {
+    if (local) {
+        localsgd_fast_kernel<<<K, 64, 0, s>>>(a, lambda, t0);
+    } else {
+        const int64_t waves = (int64_t)K * a.H;
+        const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 256 * 8));
+        mbsgd_fast_kernel<<<blocks, 256, 0, s>>>(a, K);
+    }
+}
+
+}  // namespace cocoa

@@ -122,14 +122,37 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
         wave_lds_sync();
         // x.w for each step, one lane per step, summed in stored-entry order
         double xw = 0.0;
-        if (lane < m) {
-            if (staged) {
-                for (int32_t q = 0; q < (int32_t)z; ++q) xw += prod[excl + q];
-            } else {
-                for (int64_t q = 0; q < z; ++q) xw += a.val[beg + q] * a.w[a.col[beg + q]];
+        if (STRICT) {
+            if (lane < m) {
+                if (staged) {
+                    for (int32_t q = 0; q < (int32_t)z; ++q) xw += prod[excl + q];
+                } else {
+                    for (int64_t q = 0; q < z; ++q) xw += a.val[beg + q] * a.w[a.col[beg + q]];
+                }
             }
-            mb->xw[lane] = xw;
+        } else {
+            // fast: short staged rows one lane per step; long or unstaged rows
+            // (dense data: 2,000 entries) by the whole wave, tree-summed
+            const bool wide = !staged || z > 64;
+            if (lane < m && !wide)
+                for (int32_t q = 0; q < (int32_t)z; ++q) xw += prod[excl + q];
+            uint64_t lm = __ballot(lane < m && wide);
+            while (lm) {
+                const int j = __builtin_ctzll(lm);
+                lm &= lm - 1;
+                const int64_t zj = __shfl(z, j, 64), bj = __shfl(beg, j, 64);
+                const int32_t ej = __shfl(excl, j, 64);
+                const bool sj = __shfl((int32_t)staged, j, 64) != 0;
+                double acc = 0.0;
+                if (sj)
+                    for (int32_t q = lane; q < (int32_t)zj; q += 64) acc += prod[ej + q];
+                else
+                    for (int64_t q = lane; q < zj; q += 64) acc = fma(a.val[bj + q], a.w[a.col[bj + q]], acc);
+                const double t = wave_sum(acc);
+                if (lane == j) xw = t;
+            }
         }
+        if (lane < m) mb->xw[lane] = xw;
     }
     if (lane == 0) mb->m = m;
     cursor += m;

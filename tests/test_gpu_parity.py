@@ -126,7 +126,7 @@ def test_c1_strict_run_bitwise_golden(c1, method):
         assert sha(e.alpha()) == fx["alpha_sha256"]
 
 
-@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd"])
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"])
 def test_c1_fast_run_within_tolerance(c1, method):
     tr, te = c1
     fx = _j("c1_%s.json" % method.replace("+", "plus"))
@@ -138,10 +138,12 @@ def test_c1_fast_run_within_tolerance(c1, method):
         e.round(t)
         if t in recs:
             ev = e.eval()
-            P, D = float.fromhex(recs[t]["primal"]), float.fromhex(recs[t]["dual"])
+            P = float.fromhex(recs[t]["primal"])
             assert abs(ev["primal"] - P) <= REL * abs(P)
-            assert abs(ev["dual"] - D) <= REL * abs(D)
-            assert abs(ev["gap"] - (P - D)) <= REL * abs(P)
+            if "dual" in recs[t]:
+                D = float.fromhex(recs[t]["dual"])
+                assert abs(ev["dual"] - D) <= REL * abs(D)
+                assert abs(ev["gap"] - (P - D)) <= REL * abs(P)
             assert ev["test_err_count"] == recs[t]["test_err"]
 
 
@@ -204,7 +206,7 @@ def test_edge_rows_strict_bitwise_vs_oracle(method, gamma, beta):
     assert np.array_equal(e.alpha(), run.alpha())
 
 
-@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd"])
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"])
 def test_edge_rows_fast_within_tolerance(method):
     tr = _dataset_with_edges(4)
     od = odata(tr)
@@ -216,7 +218,8 @@ def test_edge_rows_fast_within_tolerance(method):
         e.round(t)
     wr = run.w()
     assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
-    assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
+    if method in ("cocoa+", "cocoa", "mbcd"):
+        assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
 
 
 def test_empty_partition_is_an_error():
@@ -334,3 +337,22 @@ def test_fast_eval_versions_match_oracle(version, variant, monkeypatch):
     for k in ("primal", "dual", "gap"):
         assert abs(ev[k] - rv[k]) <= 1e-12 * abs(rv["primal"]), k
     assert ev["test_err_count"] == rv["test_err"]
+
+
+@pytest.mark.parametrize("method", ["mbsgd", "localsgd"])
+def test_c2_fast_sgd_matches_strict(c2, method):
+    """Full-size C5 check: the fast SGD kernels (parallel mb-SGD steps, local
+    SGD with the shrink folded into a scalar) against the strict kernels that
+    follow SGD.scala step for step."""
+    H = 677399 // 64
+    f = engine(c2, strict=False)
+    s = engine(c2, strict=True)
+    f.init(method, c2.n, 3, H, 1e-4)
+    s.init(method, c2.n, 3, H, 1e-4)
+    for t in range(1, 4):
+        f.round(t)
+        s.round(t)
+    ws, wf = s.w(), f.w()
+    assert np.max(np.abs(wf - ws)) <= REL * np.max(np.abs(ws))
+    es, ef = s.eval(), f.eval()
+    assert abs(es["primal"] - ef["primal"]) <= REL * es["primal"]
