@@ -131,7 +131,7 @@ struct cocoa_ctx {
     size_t lds_bytes = 0;
     SolverArgs sa{};
     // solver plan (v2: CoCoA+ / MbCD)
-    bool use_v2 = false;
+    bool use_v2 = false, use_plan = false;
     size_t lds2_bytes = 0;
     Solver2Args sa2{};
     DevBuf plan_beg, plan_z, plan_y, plan_q, plan_xw;
@@ -587,6 +587,14 @@ static int chain_version() {
     return (e && std::strcmp(e, "v1") == 0) ? 1 : 3;
 }
 
+// per-step plan for the v1 solver's loader: on unless COCOA_PLAN=0.  r01 on
+// MI355X: C2 9.41 -> 9.35 ms per step (plan 0.34 ms, solver -0.40 ms), C3
+// 109.6 -> 86.8 ms per step.
+static bool plan_enabled() {
+    const char* e = std::getenv("COCOA_PLAN");
+    return !(e && std::strcmp(e, "0") == 0);
+}
+
 static bool v2_enabled() {
     const char* e = std::getenv("COCOA_SOLVER");
     return e && std::strcmp(e, "v2") == 0;
@@ -666,13 +674,27 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.scaling = ctx->scaling;
 
     ctx->use_v2 = v2_enabled() && (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_MBCD);
-    if (ctx->use_v2) {
+    // v1 solver fed by the per-step plan (default; COCOA_PLAN=0 turns it off): SDCA methods only
+    ctx->use_plan = !ctx->use_v2 && plan_enabled() && is_sdca(method);
+    a.plan_beg = nullptr;
+    a.plan_z = nullptr;
+    a.plan_y = a.plan_q = a.plan_xw = nullptr;
+    if (ctx->use_v2 || ctx->use_plan) {
         const size_t steps = (size_t)std::max<int64_t>((int64_t)K * H, 1);
         ctx->plan_beg.alloc(steps * sizeof(int64_t));
         ctx->plan_z.alloc(steps * sizeof(int32_t));
         ctx->plan_y.alloc(steps * sizeof(double));
         ctx->plan_q.alloc(steps * sizeof(double));
         ctx->plan_xw.alloc(steps * sizeof(double));
+    }
+    if (ctx->use_plan) {
+        a.plan_beg = ctx->plan_beg.as<int64_t>();
+        a.plan_z = ctx->plan_z.as<int32_t>();
+        a.plan_y = ctx->plan_y.as<double>();
+        a.plan_q = ctx->plan_q.as<double>();
+        a.plan_xw = ctx->plan_xw.as<double>();
+    }
+    if (ctx->use_v2) {
         plan_solver2(ctx, ctx->max_nl);
         Solver2Args& b = ctx->sa2;
         b.row_ptr = a.row_ptr;
@@ -698,7 +720,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         b.sigma = a.sigma;
         b.scaling = a.scaling;
         b.prof = nullptr;
-    } else {
+    } else if (!ctx->use_plan) {
         ctx->plan_beg.free();
         ctx->plan_z.free();
         ctx->plan_y.free();
@@ -722,7 +744,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         c->timed(COCOA_K_SAMPLE, [&] {
             launch_sampler(c->part_ptr.as<int64_t>(), K, seed, H, c->samples.as<int32_t>(), c->jump.as<uint64_t>(), s);
         });
-        if (c->use_v2) {
+        if (c->use_v2 || c->use_plan) {
             PlanArgs pa{};
             pa.part_ptr = c->part_ptr.as<int64_t>();
             pa.samples = c->samples.as<int32_t>();
@@ -734,7 +756,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
             pa.w = c->w.as<double>();
             pa.steps = (int64_t)K * H;
             pa.H = H;
-            pa.need_xw = 1;
+            pa.need_xw = c->method != COCOA_METHOD_COCOA;  // CoCoA's w moves inside the round
             pa.beg = c->plan_beg.as<int64_t>();
             pa.z = c->plan_z.as<int32_t>();
             pa.py = c->plan_y.as<double>();
@@ -746,6 +768,8 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
                 else
                     launch_plan_fast(pa, s);
             });
+        }
+        if (c->use_v2) {
             c->timed(COCOA_K_SOLVER, [&] {
                 if (c->strict)
                     launch_solver2_strict(solver_mode(c->method), c->sa2, K, c->lds2_bytes, s);
@@ -1012,6 +1036,9 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     a.w = wb.as<double>();
     a.dw = dwb.as<double>();
     a.wloc = plus ? nullptr : wl.as<double>();
+    a.plan_beg = nullptr;  // the unit API stages its rows itself
+    a.plan_z = nullptr;
+    a.plan_y = a.plan_q = a.plan_xw = nullptr;
     a.d = d;
     a.H = local_iters;
     a.any_dup = ctx->any_dup ? 1 : 0;

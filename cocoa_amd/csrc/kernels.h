@@ -46,6 +46,14 @@ struct SolverArgs {
     const double* w;          // shared w (read-only during the round)
     double* dw;               // K_loc * d private deltaW (zero on entry)
     double* wloc;             // K_loc * d task copy of w (CoCoA) when not in LDS
+    // per-step plan (plan_kernel, one chip-wide pass per round) or null: the
+    // loader then reads each step's row extent, y, sqn and x.w with one
+    // coalesced load instead of the samples -> row_ptr -> (col, val) -> w chain
+    const int64_t* plan_beg;
+    const int32_t* plan_z;
+    const double* plan_y;
+    const double* plan_q;
+    const double* plan_xw;
     int64_t d;
     int32_t H;
     int32_t stream_cap;       // staged entries per batch buffer

@@ -22,7 +22,7 @@
 
 namespace cocoa {
 
-constexpr int kLoadUnroll = 8;  // 64-entry units each loader iteration keeps in flight
+constexpr int kLoadUnroll = 32;  // 64-entry units each loader iteration keeps in flight (a whole 2,048-entry batch)
 
 __device__ __forceinline__ int find_step(int32_t p, int32_t excl, int m) {
     // largest j < m with excl_j <= p (excl held by lane j); all lanes active
@@ -52,13 +52,24 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
     int64_t beg = 0, z = 0;
     double yv = 0.0, qv = 0.0;
     int32_t fl = 0;
+    double pxw = 0.0;
+    const bool planned = a.plan_beg != nullptr;
     if (valid) {
-        idx = a.samples[(size_t)k * H + s];
+        const size_t g = (size_t)k * H + s;
+        idx = a.samples[g];
         const int64_t gr = p0 + idx;
-        beg = a.row_ptr[gr];
-        z = a.row_ptr[gr + 1] - beg;
-        yv = a.y[gr];
-        qv = a.sqn[gr];
+        if (planned) {
+            beg = a.plan_beg[g];
+            z = a.plan_z[g];
+            yv = a.plan_y[g];
+            qv = a.plan_q[g];
+            if (MODE != MODE_COCOA) pxw = a.plan_xw[g];
+        } else {
+            beg = a.row_ptr[gr];
+            z = a.row_ptr[gr + 1] - beg;
+            yv = a.y[gr];
+            qv = a.sqn[gr];
+        }
         if (a.any_dup) fl = a.rowflags[gr];
     }
     const bool staged = z <= C;
@@ -101,7 +112,7 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
                 pv[u] = a.val[e];
             }
         }
-        if (MODE != MODE_COCOA) {
+        if (MODE != MODE_COCOA && !planned) {
 #pragma unroll
             for (int u = 0; u < kLoadUnroll; ++u) {
                 const int32_t p = base + 64 * u + lane;
@@ -114,11 +125,13 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
             if (p < T) {
                 scol[p] = pc[u];
                 sval[p] = pv[u];
-                if (MODE != MODE_COCOA) prod[p] = pv[u] * pw[u];
+                if (MODE != MODE_COCOA && !planned) prod[p] = pv[u] * pw[u];
             }
         }
     }
-    if (MODE != MODE_COCOA) {
+    if (MODE != MODE_COCOA && planned) {
+        if (lane < m) mb->xw[lane] = pxw;
+    } else if (MODE != MODE_COCOA) {
         wave_lds_sync();
         // x.w for each step, one lane per step, summed in stored-entry order
         double xw = 0.0;
@@ -433,10 +446,24 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
                 for (int u = 0; u < kRegChunks; ++u) acc = fma(ch.v[u], pd[u], acc);
                 sdot = wave_sum(acc);
             } else {
+                // long row: 4 x 64 entries per pass, all gathers of a pass in flight
                 const int32_t* sc = st.off >= 0 ? scol + st.off : a.col + uni(mb->beg[s]);
                 const double* sv = st.off >= 0 ? sval + st.off : a.val + uni(mb->beg[s]);
                 double acc = 0.0;
-                for (int32_t p = lane; p < st.z; p += 64) acc += sv[p] * vec[sc[p]];
+                for (int32_t p0 = 0; p0 < st.z; p0 += 256) {
+                    int32_t c4[4];
+                    double v4[4], g4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t p = p0 + lane + 64 * u;
+                        c4[u] = p < st.z ? sc[p] : 0;
+                        v4[u] = p < st.z ? sv[p] : 0.0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) g4[u] = vec[c4[u]];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc = fma(v4[u], g4[u], acc);
+                }
                 sdot = wave_sum(acc);
             }
         }
@@ -471,7 +498,22 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
                     if (lane == 0)
                         for (int32_t q = 0; q < st.z; ++q) vec[sc[q]] = vec[sc[q]] + sv[q] * coef;
                 } else {
-                    for (int32_t p = lane; p < st.z; p += 64) vec[sc[p]] = vec[sc[p]] + sv[p] * coef;
+                    // distinct columns: a pass's reads all go out before its writes
+                    for (int32_t p0 = 0; p0 < st.z; p0 += 256) {
+                        int32_t c4[4];
+                        double v4[4], g4[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int32_t p = p0 + lane + 64 * u;
+                            c4[u] = p < st.z ? sc[p] : -1;
+                            v4[u] = p < st.z ? sv[p] : 0.0;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) g4[u] = c4[u] >= 0 ? vec[c4[u]] : 0.0;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (c4[u] >= 0) vec[c4[u]] = fma(v4[u], coef, g4[u]);
+                    }
                 }
             }
             if (lane == 0) alv[st.r] = na;                       // CoCoA.scala:186

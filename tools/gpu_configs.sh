@@ -10,6 +10,7 @@ run() {  # name, timeout, args...
   python3 -c "import json,sys; j=json.loads(open('gpurun_out/cfg_$name.json').read().strip().splitlines()[-1]); print('$name', '%.4g upd/s' % j['value'], '%.3f ms/step' % j['ms_per_step'], 'ttg', j['time_to_gap_s'], j['rounds_to_gap'], 'solver ms %.3f' % j['kernel_ms'].get('solver', 0), 'eval ms %.3f' % j['kernel_ms'].get('eval', 0), 'cpu', (j['cpu_baseline'] or {}).get('value'))"
 }
 for m in ${METHODS:-cocoa mbcd mbsgd localsgd}; do
+  [ "$m" = none ] && continue
   run c5_$m 240 --config c2 --method $m --steps 5 --warmup 1 --gap-max-rounds 150 --cpu-seconds 5 || exit 1
 done
 run c3 400 --config c3 --steps 3 --warmup 1 --gap-max-rounds 60 --cpu-seconds 5 || exit 1
