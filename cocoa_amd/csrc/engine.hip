@@ -987,6 +987,113 @@ extern "C" int cocoa_set_alpha(cocoa_ctx* ctx, const double* alpha_in) {
     CAPI_END(ctx)
 }
 
+// ------------------------------------------------------------ checkpoint --
+namespace {
+struct CkptHeader {
+    char magic[8];
+    int32_t method, num_features, k_glob, part_begin, k_loc, local_iters;
+    int64_t n, rows;
+    double lambda, beta, gamma;
+    int32_t t, pad;
+    int64_t reserved[2];
+};
+static_assert(sizeof(CkptHeader) == 96, "checkpoint header layout");
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ULL;
+    return h;
+}
+
+CkptHeader ckpt_header(const cocoa_ctx* c, int32_t t) {
+    CkptHeader h{};
+    std::memcpy(h.magic, "COCOACK1", 8);
+    h.method = c->method;
+    h.num_features = c->d;
+    h.k_glob = c->K_glob;
+    h.part_begin = c->part_begin;
+    h.k_loc = c->K_loc;
+    h.local_iters = c->P.local_iters;
+    h.n = c->P.n;
+    h.rows = c->tr.n;
+    h.lambda = c->P.lambda;
+    h.beta = c->P.beta;
+    h.gamma = c->P.gamma;
+    h.t = t;
+    return h;
+}
+}  // namespace
+
+extern "C" int cocoa_checkpoint_save(cocoa_ctx* ctx, const char* path, int32_t t) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited, COCOA_E_STATE, "cocoa_checkpoint_save: call cocoa_init first");
+    require(path != nullptr && t >= 0, COCOA_E_ARG, "cocoa_checkpoint_save: bad argument");
+    std::vector<double> w((size_t)ctx->d), dev((size_t)ctx->d), al((size_t)std::max<int64_t>(ctx->tr.n, 1));
+    HIPCHK(hipMemcpyAsync(dev.data(), ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->tr.n)
+        HIPCHK(hipMemcpyAsync(al.data(), ctx->alpha.p, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->to_host_order(dev, w.data());
+    const CkptHeader h = ckpt_header(ctx, t);
+    uint64_t sum = 1469598103934665603ULL;
+    sum = fnv1a(sum, &h, sizeof h);
+    sum = fnv1a(sum, w.data(), sizeof(double) * w.size());
+    sum = fnv1a(sum, al.data(), sizeof(double) * (size_t)ctx->tr.n);
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    require(f != nullptr, COCOA_E_IO, std::string("cannot write checkpoint ") + tmp);
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1;
+    ok = ok && std::fwrite(w.data(), sizeof(double), w.size(), f) == w.size();
+    ok = ok && (ctx->tr.n == 0 ||
+                std::fwrite(al.data(), sizeof(double), (size_t)ctx->tr.n, f) == (size_t)ctx->tr.n);
+    ok = ok && std::fwrite(&sum, sizeof sum, 1, f) == 1;
+    ok = (std::fclose(f) == 0) && ok;
+    require(ok, COCOA_E_IO, std::string("short write on checkpoint ") + tmp);
+    require(std::rename(tmp.c_str(), path) == 0, COCOA_E_IO, std::string("cannot rename checkpoint to ") + path);
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_checkpoint_load(cocoa_ctx* ctx, const char* path, int32_t* t_out) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited, COCOA_E_STATE, "cocoa_checkpoint_load: call cocoa_init first");
+    require(path != nullptr && t_out != nullptr, COCOA_E_ARG, "cocoa_checkpoint_load: bad argument");
+    FILE* f = std::fopen(path, "rb");
+    require(f != nullptr, COCOA_E_IO, std::string("cannot open checkpoint ") + path);
+    CkptHeader h{};
+    std::vector<double> w((size_t)ctx->d), al((size_t)std::max<int64_t>(ctx->tr.n, 1));
+    uint64_t stored = 0;
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, "COCOACK1", 8) == 0;
+    const CkptHeader want = ckpt_header(ctx, h.t);
+    const bool same = ok && h.method == want.method && h.num_features == want.num_features &&
+                      h.k_glob == want.k_glob && h.part_begin == want.part_begin && h.k_loc == want.k_loc &&
+                      h.local_iters == want.local_iters && h.n == want.n && h.rows == want.rows &&
+                      h.lambda == want.lambda && h.beta == want.beta && h.gamma == want.gamma && h.t >= 0;
+    if (same) {
+        ok = std::fread(w.data(), sizeof(double), w.size(), f) == w.size();
+        ok = ok && (ctx->tr.n == 0 || std::fread(al.data(), sizeof(double), (size_t)ctx->tr.n, f) == (size_t)ctx->tr.n);
+        ok = ok && std::fread(&stored, sizeof stored, 1, f) == 1;
+    }
+    std::fclose(f);
+    require(ok, COCOA_E_IO, std::string("not a COCOACK1 checkpoint or truncated: ") + path);
+    require(same, COCOA_E_ARG,
+            std::string("checkpoint ") + path + " was written for a different problem, method or partitioning");
+    uint64_t sum = 1469598103934665603ULL;
+    sum = fnv1a(sum, &h, sizeof h);
+    sum = fnv1a(sum, w.data(), sizeof(double) * w.size());
+    sum = fnv1a(sum, al.data(), sizeof(double) * (size_t)ctx->tr.n);
+    require(sum == stored, COCOA_E_IO, std::string("checkpoint checksum mismatch: ") + path);
+    std::vector<double> dev;
+    ctx->to_device_order(w.data(), dev);
+    HIPCHK(hipMemcpyAsync(ctx->w.p, dev.data(), sizeof(double) * (size_t)ctx->d, hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->tr.n)
+        HIPCHK(hipMemcpyAsync(ctx->alpha.p, al.data(), sizeof(double) * (size_t)ctx->tr.n, hipMemcpyHostToDevice,
+                              ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *t_out = h.t;
+    CAPI_END(ctx)
+}
+
 // ------------------------------------------------- unit: CoCoA.localSDCA --
 extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t local_iters, double lambda, int32_t n,
                                 double* alpha, int32_t seed, int plus, double sigma, double* delta_w,

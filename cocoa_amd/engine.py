@@ -1,6 +1,7 @@
 """Engine: one libcocoa_hip context (one GPU, one stream) holding one rank's
 partitions.  Thin, typed wrapper over include/cocoa_capi.h."""
 import ctypes
+import os
 import json
 
 import numpy as np
@@ -106,6 +107,16 @@ class Engine:
     def set_alpha(self, a):
         a = np.ascontiguousarray(a, np.float64)
         C.check(C.lib().cocoa_set_alpha(self.h, C.f64p(a)), self.h)
+
+    def save_checkpoint(self, path, t):
+        """(t, w, alpha) of this rank to `path` (cocoa_checkpoint_save)."""
+        C.check(C.lib().cocoa_checkpoint_save(self.h, os.fsencode(path), int(t)), self.h)
+
+    def load_checkpoint(self, path):
+        """Restore w and alpha from `path`; returns the round t to resume after."""
+        t = ctypes.c_int32(0)
+        C.check(C.lib().cocoa_checkpoint_load(self.h, os.fsencode(path), ctypes.byref(t)), self.h)
+        return t.value
 
     def local_sdca(self, part, w, local_iters, lam, n, alpha, seed, plus, sigma):
         """CoCoA.localSDCA on partition `part` (CoCoA.scala:130).  w and alpha are

@@ -146,6 +146,19 @@ int cocoa_get_alpha(cocoa_ctx *ctx, double *alpha_out);   /* this rank's n_rows 
 int cocoa_set_w(cocoa_ctx *ctx, const double *w_in);
 int cocoa_set_alpha(cocoa_ctx *ctx, const double *alpha_in);
 
+/* (t, w, alpha) checkpoint of this rank.  The reference checkpoints its alpha
+ * RDD every chkptIter rounds only to truncate Spark lineage
+ * (CoCoA.scala:58-62); here the round state goes to a file so that a long run
+ * (config C4) can stop and resume.  Format "COCOACK1", little-endian: a
+ * 96-byte header (method, n, num_features, K_glob, part_begin, K_loc, rows,
+ * local_iters, lambda, beta, gamma, t), w[num_features] in original feature
+ * order, alpha[rows], then an FNV-1a 64 checksum of everything before it.
+ * Load validates the header against the context (same problem, method and
+ * partitioning; COCOA_E_ARG otherwise) and the checksum (COCOA_E_IO), sets w
+ * and alpha, and returns the round t to resume after. */
+int cocoa_checkpoint_save(cocoa_ctx *ctx, const char *path, int32_t t);
+int cocoa_checkpoint_load(cocoa_ctx *ctx, const char *path, int32_t *t_out);
+
 /* CoCoA.localSDCA (CoCoA.scala:130-192) for ONE partition of the loaded
  * training set, as a unit: w (in/out, mutated when plus == 0, like the
  * reference's alias), alpha (in/out), delta_w (out, num_features),

@@ -356,3 +356,36 @@ def test_c2_fast_sgd_matches_strict(c2, method):
     assert np.max(np.abs(wf - ws)) <= REL * np.max(np.abs(ws))
     es, ef = s.eval(), f.eval()
     assert abs(es["primal"] - ef["primal"]) <= REL * es["primal"]
+
+
+def test_checkpoint_resume_is_bitwise(c1, tmp_path):
+    """Stop after round 3, resume from the (t, w, alpha) checkpoint in a fresh
+    context: rounds 4..6 land on exactly the uninterrupted run's w and alpha."""
+    tr, te = c1
+    H = max(int(0.1 * tr.n / 4), 1)
+    a = engine(tr, te, strict=True)
+    a.init("cocoa+", tr.n, 6, H, 1e-3)
+    path = str(tmp_path / "c1.ckpt")
+    for t in range(1, 7):
+        a.round(t)
+        if t == 3:
+            a.save_checkpoint(path, t)
+    b = engine(tr, te, strict=True)
+    b.init("cocoa+", tr.n, 6, H, 1e-3)
+    t0 = b.load_checkpoint(path)
+    assert t0 == 3
+    for t in range(t0 + 1, 7):
+        b.round(t)
+    assert np.array_equal(a.w(), b.w())
+    assert np.array_equal(a.alpha(), b.alpha())
+    # a different method / partitioning is refused, a damaged file is refused
+    c = engine(tr, te, strict=True)
+    c.init("cocoa", tr.n, 6, H, 1e-3)
+    with pytest.raises(cocoa_amd.IllegalArgumentError):
+        c.load_checkpoint(path)
+    raw = bytearray(open(path, "rb").read())
+    raw[200] ^= 0xFF
+    bad = str(tmp_path / "bad.ckpt")
+    open(bad, "wb").write(bytes(raw))
+    with pytest.raises(cocoa_amd.CocoaError):
+        b.load_checkpoint(bad)
