@@ -129,6 +129,72 @@ static bool ds_alloc(cocoa_dataset* ds, int64_t n, int64_t nnz, int32_t K) {
     return ds->row_ptr && ds->col && ds->val && ds->y && ds->part_ptr;
 }
 
+// One LIBSVM line (OptUtils.scala:31-50): label rule ("+" anywhere, or the
+// integer 1 -> +1, else -1), then "index:value" tokens split on single spaces,
+// index - 1 checked against numFeatures.  Writes y, the entries and their
+// count; on a malformed line returns the reference's exception kind.
+static int parse_line(const char* b, const char* le, int64_t r, int32_t num_features, double* y, int32_t* col,
+                      double* val, int64_t* z, std::string* msg) {
+    int64_t k = 0;
+    while (b < le && java_ws(*b)) ++b;  // line.trim()
+    while (le > b && java_ws(le[-1])) --le;
+    // line.split(' '): tokens separated by single spaces; trailing empties dropped
+    const char* tok = b;
+    bool first = true;
+    for (;;) {
+        const char* te = tok;
+        while (te < le && *te != ' ') ++te;
+        if (first) {
+            const bool plus = std::memchr(tok, '+', (size_t)(te - tok)) != nullptr;
+            double lab = -1.0;
+            if (plus) {
+                lab = 1.0;
+            } else {
+                int32_t v;
+                if (!parse_int(tok, te, &v)) {
+                    *msg = "NumberFormatException: label on line " + std::to_string(r + 1);
+                    return COCOA_E_PARSE;
+                }
+                if (v == 1) lab = 1.0;
+            }
+            *y = lab;
+            first = false;
+        } else {
+            bool rest_blank = true;
+            for (const char* q = tok; q < le; ++q)
+                if (*q != ' ') {
+                    rest_blank = false;
+                    break;
+                }
+            if (rest_blank) break;
+            const char* c = (const char*)std::memchr(tok, ':', (size_t)(te - tok));
+            if (!c || c + 1 >= te || std::memchr(c + 1, ':', (size_t)(te - c - 1))) {
+                *msg = "MatchError: feature token on line " + std::to_string(r + 1);
+                return COCOA_E_PARSE;
+            }
+            int32_t idx;
+            double v;
+            if (!parse_int(tok, c, &idx) || !parse_double(c + 1, te, &v)) {
+                *msg = "NumberFormatException: feature on line " + std::to_string(r + 1);
+                return COCOA_E_PARSE;
+            }
+            const int64_t j = (int64_t)idx - 1;
+            if (j < 0 || j >= num_features) {
+                *msg = "ArrayIndexOutOfBoundsException: feature index " + std::to_string(idx) + " on line " +
+                       std::to_string(r + 1) + " (numFeatures=" + std::to_string(num_features) + ")";
+                return COCOA_E_RANGE;
+            }
+            col[k] = (int32_t)j;
+            val[k] = v;
+            ++k;
+        }
+        if (te >= le) break;
+        tok = te + 1;
+    }
+    *z = k;
+    return COCOA_OK;
+}
+
 extern "C" int cocoa_load_libsvm(const char* path, int32_t num_splits, int32_t num_features, cocoa_dataset* out) {
     if (!path || !out || num_splits < 1) return host_fail(COCOA_E_ARG, "cocoa_load_libsvm: bad argument");
     std::memset(out, 0, sizeof(*out));
@@ -147,28 +213,84 @@ extern "C" int cocoa_load_libsvm(const char* path, int32_t num_splits, int32_t n
     const int ns = (int)starts.size();
     const int K = std::min(ns, (int)num_splits);  // coalesce(numSplits)
 
-    // pass 1: line starts and nnz upper bound
-    std::vector<int64_t> line_beg;
-    int64_t colons = 0;
-    for (int64_t p = 0; p < S;) {
-        line_beg.push_back(p);
-        const char* nl = (const char*)std::memchr(buf.data() + p, '\n', (size_t)(S - p));
-        const int64_t e = nl ? nl - buf.data() : S;
-        for (int64_t q = p; q < e; ++q) colons += buf[(size_t)q] == ':';
-        p = e + 1;
+    // Multithreaded ingest (one pass per stage, threads over byte / line
+    // ranges); results and error reporting are those of the sequential parse:
+    // the first malformed line in file order raises.
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
+                                                                 S / (1 << 20) + 1}));
+    auto run = [&](auto&& fn) {
+        std::vector<std::thread> th;
+        for (int i = 1; i < nt; ++i) th.emplace_back(fn, i);
+        fn(0);
+        for (auto& x : th) x.join();
+    };
+    // pass 1: line starts and per-line ':' counts (an upper bound of the line's nnz)
+    std::vector<std::vector<int64_t>> lb(nt), lc(nt);
+    run([&](int i) {
+        const int64_t c0 = S * i / nt, c1 = S * (i + 1) / nt;
+        int64_t p = c0;
+        if (p > 0) {  // first line starting inside [c0, c1)
+            const char* nl = (const char*)std::memchr(buf.data() + p - 1, '\n', (size_t)(S - p + 1));
+            p = nl ? (nl - buf.data()) + 1 : S;
+        }
+        while (p < c1) {
+            const char* nl = (const char*)std::memchr(buf.data() + p, '\n', (size_t)(S - p));
+            const int64_t e = nl ? nl - buf.data() : S;
+            int64_t cc = 0;
+            for (int64_t q = p; q < e; ++q) cc += buf[(size_t)q] == ':';
+            lb[(size_t)i].push_back(p);
+            lc[(size_t)i].push_back(cc);
+            p = e + 1;
+        }
+    });
+    std::vector<int64_t> line_beg, cap{0};
+    for (int i = 0; i < nt; ++i) {
+        line_beg.insert(line_beg.end(), lb[(size_t)i].begin(), lb[(size_t)i].end());
+        for (int64_t c : lc[(size_t)i]) cap.push_back(cap.back() + c);
+        std::vector<int64_t>().swap(lb[(size_t)i]);
+        std::vector<int64_t>().swap(lc[(size_t)i]);
     }
     const int64_t n = (int64_t)line_beg.size();
-    if (!ds_alloc(out, n, colons, K)) return host_fail(COCOA_E_ARG, "out of host memory");
+    if (!ds_alloc(out, n, cap.back(), K)) return host_fail(COCOA_E_ARG, "out of host memory");
     out->n_rows = n;
     out->num_features = num_features;
     out->num_parts = K;
 
+    // pass 2: parse lines in parallel, each into its slot at cap[r]
+    std::vector<int64_t> zr((size_t)n, 0);
+    std::vector<int64_t> bad_line((size_t)nt, n);
+    std::vector<int> bad_code((size_t)nt, COCOA_OK);
+    std::vector<std::string> bad_msg((size_t)nt);
+    run([&](int i) {
+        const int64_t r0 = n * i / nt, r1 = n * (i + 1) / nt;
+        for (int64_t r = r0; r < r1; ++r) {
+            const int64_t p = line_beg[(size_t)r];
+            const int64_t e = r + 1 < n ? line_beg[(size_t)r + 1] - 1 : S;
+            std::string msg;
+            const int rc = parse_line(buf.data() + p, buf.data() + e, r, num_features, out->y + r,
+                                      out->col + cap[(size_t)r], out->val + cap[(size_t)r], &zr[(size_t)r], &msg);
+            if (rc != COCOA_OK) {
+                bad_line[(size_t)i] = r;
+                bad_code[(size_t)i] = rc;
+                bad_msg[(size_t)i] = msg;
+                return;
+            }
+        }
+    });
+    for (int i = 0; i < nt; ++i)
+        if (bad_code[(size_t)i] != COCOA_OK) {  // threads own increasing line ranges: the first is the earliest
+            cocoa_dataset_free(out);
+            return host_fail(bad_code[(size_t)i], bad_msg[(size_t)i]);
+        }
+
+    // pass 3: partitions (Hadoop split of the line's first byte), row_ptr, and
+    // compaction of the slots (in place, moving left, only where a line had
+    // fewer entries than ':' characters)
     int64_t nnz = 0;
     int split = 0;
     out->row_ptr[0] = 0;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t p = line_beg[(size_t)r];
-        const int64_t e = r + 1 < n ? line_beg[(size_t)r + 1] - 1 : S;
         while (split + 1 < ns && p >= starts[(size_t)split + 1]) ++split;  // split holding the line's 1st byte
         int part = split;
         if (ns > K) {  // CoalescedRDD without locality: consecutive ranges of splits
@@ -176,64 +298,12 @@ extern "C" int cocoa_load_libsvm(const char* path, int32_t num_splits, int32_t n
             while (part + 1 < K && (int64_t)split >= ((int64_t)(part + 1) * ns) / K) ++part;
         }
         out->part_ptr[part + 1]++;
-        const char* b = buf.data() + p;
-        const char* le = buf.data() + e;
-        while (b < le && java_ws(*b)) ++b;  // line.trim()
-        while (le > b && java_ws(le[-1])) --le;
-        // line.split(' '): tokens separated by single spaces; trailing empties dropped
-        const char* tok = b;
-        bool first = true;
-        for (;;) {
-            const char* te = tok;
-            while (te < le && *te != ' ') ++te;
-            if (first) {
-                const bool plus = std::memchr(tok, '+', (size_t)(te - tok)) != nullptr;
-                double lab = -1.0;
-                if (plus) {
-                    lab = 1.0;
-                } else {
-                    int32_t v;
-                    if (!parse_int(tok, te, &v)) {
-                        cocoa_dataset_free(out);
-                        return host_fail(COCOA_E_PARSE, "NumberFormatException: label on line " + std::to_string(r + 1));
-                    }
-                    if (v == 1) lab = 1.0;
-                }
-                out->y[r] = lab;
-                first = false;
-            } else {
-                bool rest_blank = true;
-                for (const char* q = tok; q < le; ++q)
-                    if (*q != ' ') {
-                        rest_blank = false;
-                        break;
-                    }
-                if (rest_blank) break;
-                const char* c = (const char*)std::memchr(tok, ':', (size_t)(te - tok));
-                if (!c || c + 1 >= te || std::memchr(c + 1, ':', (size_t)(te - c - 1))) {
-                    cocoa_dataset_free(out);
-                    return host_fail(COCOA_E_PARSE, "MatchError: feature token on line " + std::to_string(r + 1));
-                }
-                int32_t idx;
-                double v;
-                if (!parse_int(tok, c, &idx) || !parse_double(c + 1, te, &v)) {
-                    cocoa_dataset_free(out);
-                    return host_fail(COCOA_E_PARSE, "NumberFormatException: feature on line " + std::to_string(r + 1));
-                }
-                const int64_t j = (int64_t)idx - 1;
-                if (j < 0 || j >= num_features) {
-                    cocoa_dataset_free(out);
-                    return host_fail(COCOA_E_RANGE, "ArrayIndexOutOfBoundsException: feature index " + std::to_string(idx) +
-                                                        " on line " + std::to_string(r + 1) + " (numFeatures=" +
-                                                        std::to_string(num_features) + ")");
-                }
-                out->col[nnz] = (int32_t)j;
-                out->val[nnz] = v;
-                ++nnz;
-            }
-            if (te >= le) break;
-            tok = te + 1;
+        const int64_t z = zr[(size_t)r], src = cap[(size_t)r];
+        if (src != nnz && z > 0) {
+            std::memmove(out->col + nnz, out->col + src, sizeof(int32_t) * (size_t)z);
+            std::memmove(out->val + nnz, out->val + src, sizeof(double) * (size_t)z);
         }
+        nnz += z;
         out->row_ptr[r + 1] = nnz;
     }
     for (int k = 1; k <= K; ++k) out->part_ptr[k] += out->part_ptr[k - 1];
