@@ -130,3 +130,47 @@ def test_java_double_strings():
     assert j(0.1) == "0.1" and j(1e-4) == "1.0E-4" and j(0.001) == "0.001" and j(1e7) == "1.0E7"
     assert j(9999999.0) == "9999999.0" and j(-0.025) == "-0.025" and j(2.5e-10) == "2.5E-10"
     assert j(0.0) == "0.0" and j(float("nan")) == "NaN" and j(12345678.9) == "1.23456789E7"
+
+
+def _big_file(tmp_path, copies=6):
+    """The demo train file repeated: > 1 MB, so the loader runs its
+    multithreaded line split / parse / compaction passes."""
+    raw = open(TRAIN, "rb").read()
+    p = tmp_path / "big.dat"
+    p.write_bytes(raw * copies)
+    return str(p), raw
+
+
+@pytest.mark.parametrize("K", [1, 4, 9])
+def test_loader_multithreaded_matches_oracle(tmp_path, K):
+    fn, raw = _big_file(tmp_path)
+    assert len(raw) * 6 > (1 << 21)
+    a = cocoa_amd.load_libsvm(fn, K, 9947)
+    b = oracle.Data.load_libsvm(fn, K, 9947)
+    for f in ("row_ptr", "col", "val", "y", "part_ptr"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_loader_multithreaded_reports_first_bad_line(tmp_path):
+    fn, raw = _big_file(tmp_path)
+    lines = open(fn, "rb").read().split(b"\n")
+    n = len(lines)
+    lines[int(n * 0.7)] = b"1 7:1 0:2"        # index 0 -> ArrayIndexOutOfBounds, later in the file
+    lines[int(n * 0.3)] = b"1 3:1 x:4"        # NumberFormatException, earlier: this one is reported
+    bad = tmp_path / "bad.dat"
+    bad.write_bytes(b"\n".join(lines))
+    with pytest.raises(cocoa_amd.NumberFormatError, match="line %d" % (int(n * 0.3) + 1)):
+        cocoa_amd.load_libsvm(str(bad), 4, 9947)
+
+
+def test_loader_multithreaded_trailing_blanks(tmp_path):
+    """Lines ending in a blank token (line.trim() then split(' ')) through the
+    multithreaded passes, against the oracle's sequential parse."""
+    fn, raw = _big_file(tmp_path, 5)
+    text = open(fn, "rb").read().replace(b"\n", b" \n", 50)
+    p = tmp_path / "ws.dat"
+    p.write_bytes(text)
+    a = cocoa_amd.load_libsvm(str(p), 3, 9947)
+    b = oracle.Data.load_libsvm(str(p), 3, 9947)
+    for f in ("row_ptr", "col", "val", "y", "part_ptr"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
