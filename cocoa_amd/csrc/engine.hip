@@ -135,6 +135,10 @@ struct cocoa_ctx {
     size_t lds2_bytes = 0;
     Solver2Args sa2{};
     DevBuf plan_beg, plan_z, plan_y, plan_q, plan_xw;
+    // x.w of every train row for the current w, written by the fast eval pass
+    // (eval v4) and reused by the next round's plan; false once w moves
+    DevBuf row_xw;
+    bool xw_cached = false;
     int32_t max_z = 0;
 
     // stats
@@ -625,6 +629,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     }
     hipStream_t s = ctx->stream;
     ctx->w.alloc(sizeof(double) * (size_t)d);
+    ctx->xw_cached = false;
+    ctx->row_xw.alloc(sizeof(double) * (size_t)std::max<int64_t>(ctx->tr.n, 1));
     std::vector<double> wdev;
     if (w_init) {
         ctx->to_device_order(w_init, wdev);
@@ -757,6 +763,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
             pa.steps = (int64_t)K * H;
             pa.H = H;
             pa.need_xw = c->method != COCOA_METHOD_COCOA;  // CoCoA's w moves inside the round
+            pa.xw_cache = (c->xw_cached && !c->strict) ? c->row_xw.as<double>() : nullptr;
             pa.beg = c->plan_beg.as<int64_t>();
             pa.z = c->plan_z.as<int32_t>();
             pa.py = c->plan_y.as<double>();
@@ -808,6 +815,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         launch_fold(c->dw.as<double>(), K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply,
                     c->d_inv.as<int32_t>(), s);
     });
+    c->xw_cached = false;  // w moves this round (scale / fused apply / the caller's apply)
 }
 
 extern "C" int cocoa_round_local(cocoa_ctx* ctx, int32_t t) {
@@ -836,6 +844,7 @@ extern "C" int cocoa_round_apply(cocoa_ctx* ctx) {
     ctx->timed(COCOA_K_APPLY, [&] {
         launch_apply(ctx->w.as<double>(), ctx->dw_sum, ctx->d, ctx->mult, ctx->d_inv.as<int32_t>(), ctx->stream);
     });
+    ctx->xw_cached = false;
     CAPI_END(ctx)
 }
 
@@ -905,7 +914,10 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
                 e.t_tiles = ctx->has_test ? ctx->t_tiles4k.as<int64_t>() : nullptr;
                 e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles4k : 0;
             }
+            const bool exact = var == 0 || var == 1 || var == 3 || var == 8;  // the rest are timing diagnostics
+            e.row_xw = exact ? ctx->row_xw.as<double>() : nullptr;
             launch_eval4(var, e, eval4_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
+            ctx->xw_cached = exact;  // the next round's plan reuses these x.w (stream order)
         }
         else
             launch_eval2(eval_version(), e, eval2_blocks(eval_version(), e.n_tiles, e.n_t_tiles), ctx->stream);
@@ -974,6 +986,7 @@ extern "C" int cocoa_set_w(cocoa_ctx* ctx, const double* w_in) {
     ctx->to_device_order(w_in, dev);
     HIPCHK(hipMemcpyAsync(ctx->w.p, dev.data(), sizeof(double) * (size_t)ctx->d, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->xw_cached = false;
     CAPI_END(ctx)
 }
 
@@ -1090,6 +1103,7 @@ extern "C" int cocoa_checkpoint_load(cocoa_ctx* ctx, const char* path, int32_t* 
         HIPCHK(hipMemcpyAsync(ctx->alpha.p, al.data(), sizeof(double) * (size_t)ctx->tr.n, hipMemcpyHostToDevice,
                               ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->xw_cached = false;
     *t_out = h.t;
     CAPI_END(ctx)
 }

@@ -142,6 +142,7 @@ struct PlanArgs {
     int64_t steps;            // K_loc * H
     int32_t H;
     int32_t need_xw;
+    const double* xw_cache;   // per-row x.w of the current w from the last fast eval, or null
     int64_t* beg;
     int32_t* z;
     double* py;
@@ -180,6 +181,7 @@ struct EvalArgs {
     double* partials;         // [blocks][4] fast; per-row scratch strict
     double* out;              // [4]: hinge_sum, alpha_sum, w_sq(norm^2 via sqrt), test_err_count
     double* row_scratch;      // n doubles (strict)
+    double* row_xw;           // n doubles or null: eval v4 also stores each train row's x.w
 };
 
 // fast translation unit

@@ -383,8 +383,12 @@ __global__ __launch_bounds__(BLOCK) void eval_v4_kernel(EvalArgs a) {
             for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += wg(vl[q], cl[q]);
             const double dot = block_sum_n<BLOCK>(acc, red);
             if (tid == 0) {
-                if (!test) hinge += jmax(1 - yy[r0] * dot, 0.0);
-                else err += (dot * yy[r0] > 0) ? 0.0 : 1.0;
+                if (!test) {
+                    hinge += jmax(1 - yy[r0] * dot, 0.0);
+                    if (a.row_xw) a.row_xw[r0] = dot;
+                } else {
+                    err += (dot * yy[r0] > 0) ? 0.0 : 1.0;
+                }
             }
             continue;
         }
@@ -427,8 +431,12 @@ __global__ __launch_bounds__(BLOCK) void eval_v4_kernel(EvalArgs a) {
             for (int q = b + sub; q < e; q += 16) acc += prod[q];
             const double dot = row16_sum(acc);
             if (sub == 0) {
-                if (!test) hinge += jmax(1 - yy[r0 + r] * dot, 0.0);
-                else err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+                if (!test) {
+                    hinge += jmax(1 - yy[r0 + r] * dot, 0.0);
+                    if (a.row_xw) a.row_xw[r0 + r] = dot;
+                } else {
+                    err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+                }
             }
         }
         __syncthreads();

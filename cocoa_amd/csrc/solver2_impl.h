@@ -522,7 +522,9 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     const int64_t gr = a.part_ptr[k] + a.samples[gg];
     const int64_t b = a.row_ptr[gr], e = a.row_ptr[gr + 1];
     double xw = 0.0;
-    if (a.need_xw) {
+    if (a.need_xw && a.xw_cache) {
+        xw = valid ? a.xw_cache[gr] : 0.0;  // the last eval pass already formed x.w for this w
+    } else if (a.need_xw) {
         if (STRICT) {
             for (int64_t q = b; q < e; ++q) xw += a.val[q] * a.w[a.col[q]];
         } else {
