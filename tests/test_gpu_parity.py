@@ -389,3 +389,59 @@ def test_checkpoint_resume_is_bitwise(c1, tmp_path):
     open(bad, "wb").write(bytes(raw))
     with pytest.raises(cocoa_amd.CocoaError):
         b.load_checkpoint(bad)
+
+
+@pytest.mark.parametrize("strict", [True, False])
+def test_two_rank_split_round_in_one_process(c1, strict):
+    """The N>1 data path on one GPU without a process group: two engines own
+    partition blocks [0,2) and [2,4) of C1 (cocoa_set_train part_begin /
+    num_parts_global), each runs cocoa_round_local into a torch-owned deltaW
+    sum, the sums are added (what the RCCL all-reduce does), then every rank
+    runs cocoa_round_apply; objectives go through cocoa_eval_finish with the
+    summed scalars (DistributedCoCoA.eval).  Against a single-process oracle
+    run: equal up to the re-association of the cross-rank sum."""
+    import torch
+    tr, te = c1
+    H, lam, Kg = 50, 1e-3, 4
+    engines, sums = [], []
+    for r in range(2):
+        k0, k1 = 2 * r, 2 * r + 2
+        r0, r1 = int(tr.part_ptr[k0]), int(tr.part_ptr[k1])
+        sh = tr.row_range(r0, r1)
+        sh.part_ptr = (tr.part_ptr[k0:k1 + 1] - r0).astype(np.int64)
+        e = Engine(strict=strict)
+        e.set_train(sh, part_begin=k0, num_parts_global=Kg)
+        t0, t1 = (0, 300) if r == 0 else (300, te.n)
+        e.set_test(te.row_range(t0, t1))
+        e.init("cocoa+", tr.n, 6, H, lam)
+        buf = torch.zeros(tr.num_features, dtype=torch.float64, device="cuda")
+        e.set_dw_sum_buffer(buf.data_ptr())
+        engines.append(e)
+        sums.append(buf)
+    run = oracle.Run(odata(tr), "cocoa+", tr.n, H, lam)
+    for t in range(1, 7):
+        run.round(t)
+        for e in engines:
+            e.round_local(t)
+            e.sync()
+        torch.cuda.synchronize()
+        tot = sums[0] + sums[1]
+        for b in sums:
+            b.copy_(tot)
+        torch.cuda.synchronize()
+        for e in engines:
+            e.round_apply()
+            e.sync()
+    w0, w1, wr = engines[0].w(), engines[1].w(), run.w()
+    assert np.array_equal(w0, w1)                      # identical bytes on every rank
+    assert np.max(np.abs(w0 - wr)) <= REL * np.max(np.abs(wr))
+    a = np.concatenate([engines[0].alpha(), engines[1].alpha()])
+    assert np.max(np.abs(a - run.alpha())) <= REL
+    evs = [e.eval() for e in engines]
+    fin = engines[0].eval_finish(sum(v["hinge_sum"] for v in evs), sum(v["alpha_sum"] for v in evs),
+                                 evs[0]["w_sqnorm"], sum(v["test_err_count"] for v in evs),
+                                 sum(v["test_rows"] for v in evs))
+    rv = run.eval(odata(te))
+    assert abs(fin["primal"] - rv["primal"]) <= REL * abs(rv["primal"])
+    assert abs(fin["gap"] - rv["gap"]) <= REL * abs(rv["primal"])
+    assert fin["test_err_count"] == rv["test_err"]
