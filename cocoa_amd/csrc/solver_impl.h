@@ -93,21 +93,40 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
         }
     }
     const int32_t T = __shfl(incl, m - 1, 64);
+    // Owner step of every staged position: step j marks the start of its row
+    // (scol[excl_j] = j), and a DPP prefix-max over each 64-position unit (plus
+    // the previous unit's last owner) spreads the marks; the marks are then
+    // overwritten by the entries.  No per-position search.
+    for (int32_t q = lane; q < T; q += 64) scol[q] = -1;
+    wave_lds_sync();
+    if (lane < m && zz > 0) scol[excl] = lane;
+    wave_lds_sync();
+    int32_t carry = 0;
     // stream the batch's entries: 64 consecutive packed positions per unit
     for (int32_t base = 0; base < T; base += 64 * kLoadUnroll) {
         int32_t pc[kLoadUnroll];
         double pv[kLoadUnroll], pw[kLoadUnroll];
+        int32_t own[kLoadUnroll];
 #pragma unroll
         for (int u = 0; u < kLoadUnroll; ++u) {
             const int32_t p = base + 64 * u + lane;
-            const int32_t pq = p < T ? p : T - 1;
-            const int j = find_step(pq, excl, m);
-            const int64_t bj = __shfl(beg, j, 64);
-            const int32_t ej = __shfl(excl, j, 64);
+            own[u] = p < T ? scol[p] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kLoadUnroll; ++u) {
+            if (base + 64 * u < T) {
+                own[u] = wave_incl_max(max(own[u], carry));
+                carry = __builtin_amdgcn_readlane(own[u], 63);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kLoadUnroll; ++u) {
+            const int32_t p = base + 64 * u + lane;
             pc[u] = 0;
             pv[u] = 0.0;
             if (p < T) {
-                const int64_t e = bj + (pq - ej);
+                const int j = own[u];
+                const int64_t e = mb->beg[j] + (p - mb->off[j]);
                 pc[u] = a.col[e];
                 pv[u] = a.val[e];
             }

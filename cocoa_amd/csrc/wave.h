@@ -62,6 +62,19 @@ __device__ __forceinline__ double wave_sum(double x) {
     return readlane_d(x, 63);
 }
 
+// Inclusive prefix max of an int over the wave in lane order (all lanes
+// active; values >= -1): row_shr steps inside each 16-lane row, then the
+// row_bcast:15 / row_bcast:31 carries between rows.  DPP only, no LDS.
+__device__ __forceinline__ int32_t wave_incl_max(int32_t x) {
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xF, 0xF, false));  // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xF, 0xF, false));  // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xF, 0xF, false));  // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xF, 0xF, false));  // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xA, 0xF, false));  // row_bcast:15 -> rows 1, 3
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xC, 0xF, false));  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 // Inclusive prefix sum of an int over the wave (all lanes active).
 __device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
     const int l = lane_id();
