@@ -462,7 +462,11 @@ static void plan_solver(cocoa_ctx* c) {
     SolverArgs& a = c->sa;
     size_t off = 0;
     const size_t vec_bytes = align16(sizeof(double) * (size_t)c->d);
-    const size_t cap = kStreamCap;
+    // long rows (dense data, C3: 2,000 entries) would leave one row per batch and
+    // make the loader's per-batch latency the bound: double the stream instead
+    // (alpha then moves to HBM when it no longer fits; the chain prefetches it)
+    const double zavg = c->tr.n ? (double)c->tr.nnz / (double)c->tr.n : 0.0;
+    const size_t cap = zavg * 4 > (double)kStreamCap ? 2 * (size_t)kStreamCap : (size_t)kStreamCap;
     const size_t fixed = 2 * align16(cap * 4) + 2 * align16(cap * 8) + 2 * align16(sizeof(BatchMeta)) +
                          align16(cap * 8) + align16(sizeof(double) * kRegChunks * 64);
     size_t avail = kLdsMax - fixed;

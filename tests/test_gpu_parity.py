@@ -445,3 +445,35 @@ def test_two_rank_split_round_in_one_process(c1, strict):
     assert abs(fin["primal"] - rv["primal"]) <= REL * abs(rv["primal"])
     assert abs(fin["gap"] - rv["gap"]) <= REL * abs(rv["primal"])
     assert fin["test_err_count"] == rv["test_err"]
+
+
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd"])
+@pytest.mark.parametrize("strict", [True, False])
+def test_dense_rows_double_stream(method, strict):
+    """Dense rows (C3-like, average z > 512): the solver plan doubles the LDS
+    entry stream and keeps alpha in HBM.  Strict stays bitwise, fast within
+    1e-9 of the oracle."""
+    rng = np.random.default_rng(5)
+    n, d = 3200, 1500                    # 1,600-row partitions: alpha no longer fits next to the stream
+    z = rng.integers(900, 1500, size=n)
+    cols = [np.sort(rng.choice(d, size=int(k), replace=False)).astype(np.int32) for k in z]
+    vals = [rng.standard_normal(int(k)) / np.sqrt(k) for k in z]
+    row_ptr = np.concatenate([[0], np.cumsum(z)]).astype(np.int64)
+    y = np.where(rng.random(n) < 0.5, 1.0, -1.0)
+    tr = LabeledData(row_ptr, np.concatenate(cols), np.concatenate(vals), y,
+                     np.array([0, 1600, 3200], np.int64), d)
+    e = engine(tr, strict=strict)
+    e.init(method, n, 4, 100, 1e-3, 1.0, 1.0, 1, 3)
+    plan = e.plan()
+    assert plan["stream_cap"] == 4096 and plan["alpha_lds"] == 0
+    run = oracle.Run(odata(tr), method, n, 100, 1e-3, seed=3)
+    for t in range(1, 5):
+        e.round(t)
+        run.round(t)
+    if strict:
+        assert np.array_equal(e.w(), run.w())
+        assert np.array_equal(e.alpha(), run.alpha())
+    else:
+        wr = run.w()
+        assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+        assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
