@@ -449,11 +449,13 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
         double pd[kRegChunks];
         if (MODE == MODE_PLUS && regs) {
 #pragma unroll
-            for (int u = 0; u < kRegChunks; ++u) pd[u] = u < nch ? vec[ch.c[u]] : 0.0;
+            for (int u = 0; u < kRegChunks; ++u) pd[u] = vec[ch.c[u]];  // chunks past z: the row's last column, v = 0
         }
         // 2. ... then the next step's staged inputs (independent of the chain)
-        if (s + 1 < m) {
-            nm = read_meta3(mb, s + 1, alv);
+        {
+            // the last step re-reads its own inputs (unused) instead of branching
+            const int s1 = s + 1 < m ? s + 1 : s;
+            nm = read_meta3(mb, s1, alv);
             read_chunks3(scol, sval, nm, nc);
         }
         const double aa = st.aa;
