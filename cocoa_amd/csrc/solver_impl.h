@@ -440,76 +440,86 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
     Meta3 nm = read_meta3(mb, 0, alv);
     Chunks3 nc;
     read_chunks3(scol, sval, nm, nc);
-    for (int s = 0; s < m; ++s) {
-        const Meta3 st = nm;
-        const Chunks3 ch = nc;
-        const int nch = (st.z + 63) >> 6;
-        const bool regs = st.off >= 0 && nch <= kRegChunks && (st.fl & 1) == 0;
-        // 1. the dependent gather of this step goes out first ...
-        double pd[kRegChunks];
-        if (MODE == MODE_PLUS && regs) {
-#pragma unroll
-            for (int u = 0; u < kRegChunks; ++u) pd[u] = vec[ch.c[u]];  // chunks past z: the row's last column, v = 0
-        }
-        // 2. ... then the next step's staged inputs (independent of the chain)
-        {
-            // the last step re-reads its own inputs (unused) instead of branching
-            const int s1 = s + 1 < m ? s + 1 : s;
-            nm = read_meta3(mb, s1, alv);
-            read_chunks3(scol, sval, nm, nc);
-        }
+    // CoCoA.scala:159-186 / MinibatchCD.scala:104-123, branch-free
+    auto rule = [&](const Meta3& st, double sdot, double& na, double& coef) -> bool {
         const double aa = st.aa;
-        double sdot = 0.0;
-        if (MODE == MODE_PLUS) {
-            if (regs) {
-                double acc = 0.0;
-#pragma unroll
-                for (int u = 0; u < kRegChunks; ++u) acc = fma(ch.v[u], pd[u], acc);
-                sdot = wave_sum(acc);
-            } else {
-                // long row: 4 x 64 entries per pass, all gathers of a pass in flight
-                const int32_t* sc = st.off >= 0 ? scol + st.off : a.col + uni(mb->beg[s]);
-                const double* sv = st.off >= 0 ? sval + st.off : a.val + uni(mb->beg[s]);
-                double acc = 0.0;
-                for (int32_t p0 = 0; p0 < st.z; p0 += 256) {
-                    int32_t c4[4];
-                    double v4[4], g4[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int32_t p = p0 + lane + 64 * u;
-                        c4[u] = p < st.z ? sc[p] : 0;
-                        v4[u] = p < st.z ? sv[p] : 0.0;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) g4[u] = vec[c4[u]];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) acc = fma(v4[u], g4[u], acc);
-                }
-                sdot = wave_sum(acc);
-            }
-        }
-        // CoCoA.scala:159-186 / MinibatchCD.scala:104-123, branch-free
         const double grad = MODE == MODE_PLUS ? (st.y * (st.xw + sigma * sdot) - 1.0) * lam_n
                                               : (st.y * st.xw - 1.0) * lam_n;
         const double proj = aa <= 0.0 ? fmin(grad, 0.0) : (aa >= 1.0 ? fmax(grad, 0.0) : grad);
         const bool go = proj != 0.0;
         const double qii = MODE == MODE_PLUS ? st.q * sigma : st.q;
         const double nt = fmin(fmax(aa - grad * st.rq, 0.0), 1.0);
-        const double na = go ? (qii != 0.0 ? nt : 1.0) : aa;
-        const double coef = (st.y * (na - aa)) * inv_lam_n;
+        na = go ? (qii != 0.0 ? nt : 1.0) : aa;
+        coef = (st.y * (na - aa)) * inv_lam_n;
+        return go;
+    };
+    auto next = [&](int s) {
+        // the last step re-reads its own inputs (unused) instead of branching
+        nm = read_meta3(mb, s + 1 < m ? s + 1 : s, alv);
+        read_chunks3(scol, sval, nm, nc);
+    };
+    for (int s = 0; s < m; ++s) {
+        const Meta3 st = nm;
+        const Chunks3 ch = nc;
+        const int nch = (st.z + 63) >> 6;
+        const bool regs = st.off >= 0 && nch <= kRegChunks && (st.fl & 1) == 0;
+        double na, coef;
+        if (MODE == MODE_PLUS && regs) {
+            // CoCoA+ register path, one uniform branch per step: the dependent
+            // gather goes out first (chunks past z hit the row's last column,
+            // v = 0), then the next step's staged inputs
+            double pd[kRegChunks];
+#pragma unroll
+            for (int u = 0; u < kRegChunks; ++u) pd[u] = vec[ch.c[u]];
+            next(s);
+            double acc = 0.0;
+#pragma unroll
+            for (int u = 0; u < kRegChunks; ++u) acc = fma(ch.v[u], pd[u], acc);
+            const bool go = rule(st, wave_sum(acc), na, coef);
+            if (s + 1 < m && nm.r == st.r) nm.aa = na;           // same row sampled twice in a row
+            if (uni((int32_t)go)) {
+#pragma unroll
+                for (int u = 0; u < kRegChunks; ++u)
+                    if (u < nch && lane + 64 * u < st.z) vec[ch.c[u]] = fma(ch.v[u], coef, pd[u]);  // deltaW += update
+                if (lane == 0) alv[st.r] = na;                   // CoCoA.scala:186
+            }
+            continue;
+        }
+        next(s);
+        double sdot = 0.0;
+        if (MODE == MODE_PLUS) {
+            // long row: 4 x 64 entries per pass, all gathers of a pass in flight
+            const int32_t* sc = st.off >= 0 ? scol + st.off : a.col + uni(mb->beg[s]);
+            const double* sv = st.off >= 0 ? sval + st.off : a.val + uni(mb->beg[s]);
+            double acc = 0.0;
+            for (int32_t p0 = 0; p0 < st.z; p0 += 256) {
+                int32_t c4[4];
+                double v4[4], g4[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int32_t p = p0 + lane + 64 * u;
+                    c4[u] = p < st.z ? sc[p] : 0;
+                    v4[u] = p < st.z ? sv[p] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) g4[u] = vec[c4[u]];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc = fma(v4[u], g4[u], acc);
+            }
+            sdot = wave_sum(acc);
+        }
+        const bool go = rule(st, sdot, na, coef);
         if (s + 1 < m && nm.r == st.r) nm.aa = na;               // same row sampled twice in a row
         if (uni((int32_t)go)) {
             if (regs) {
+                // MbCD register path: atomic adds into deltaW
 #pragma unroll
                 for (int u = 0; u < kRegChunks; ++u) {
                     if (u < nch && lane + 64 * u < st.z) {
-                        if (MODE == MODE_PLUS) {
-                            vec[ch.c[u]] = fma(ch.v[u], coef, pd[u]);  // deltaW += update
-                        } else if (VEC_LDS) {
+                        if (VEC_LDS)
                             atomicAdd(vec + ch.c[u], ch.v[u] * coef);
-                        } else {
+                        else
                             unsafeAtomicAdd(vec + ch.c[u], ch.v[u] * coef);
-                        }
                     }
                 }
             } else {
