@@ -101,6 +101,8 @@ struct cocoa_ctx {
     // row tiles of the fast evaluation pass
     DevBuf tiles, t_tiles, tiles4k, t_tiles4k;  // kEvalTile and 4096-entry tiles (eval v4)
     int64_t n_tiles = 0, n_t_tiles = 0, n_tiles4k = 0, n_t_tiles4k = 0;
+    DevBuf tilesw[3], t_tilesw[3];  // wave tiles (eval v6), caps 256 / 512 / 1024 entries
+    int64_t n_tilesw[3] = {0, 0, 0}, n_t_tilesw[3] = {0, 0, 0};
     // device feature order (see cocoa_set_train)
     std::vector<int32_t> perm, inv;
     std::vector<int64_t> n_hot_nnz;
@@ -419,6 +421,7 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s);
     ctx->n_tiles4k = make_tiles(row_ptr, n_rows, ctx->tiles4k, s, 4096);
+    for (int i = 0; i < 3; ++i) ctx->n_tilesw[i] = make_tiles(row_ptr, n_rows, ctx->tilesw[i], s, 256 << i);
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
     CAPI_END(ctx)
@@ -442,6 +445,7 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s);
     ctx->n_t_tiles4k = make_tiles(row_ptr, n_rows, ctx->t_tiles4k, s, 4096);
+    for (int i = 0; i < 3; ++i) ctx->n_t_tilesw[i] = make_tiles(row_ptr, n_rows, ctx->t_tilesw[i], s, 256 << i);
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     if (ctx->inited) {
@@ -584,6 +588,7 @@ static int eval_version() {
     if (e && std::strcmp(e, "v1") == 0) return 1;
     if (e && std::strcmp(e, "v2") == 0) return 2;
     if (e && std::strcmp(e, "v3") == 0) return 3;
+    if (e && std::strcmp(e, "v6") == 0) return 6;
     return 4;
 }
 
@@ -922,8 +927,18 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
             e.row_xw = exact ? ctx->row_xw.as<double>() : nullptr;
             launch_eval4(var, e, eval4_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
             ctx->xw_cached = exact;  // the next round's plan reuses these x.w (stream order)
-        }
-        else
+        } else if (eval_version() == 6) {
+            const char* ev = std::getenv("COCOA_EVAL6");
+            const int var = ev ? std::atoi(ev) : 0;
+            const int ti = eval6_tile(var) == 256 ? 0 : eval6_tile(var) == 512 ? 1 : 2;
+            e.tiles = ctx->tilesw[ti].as<int64_t>();
+            e.n_tiles = ctx->n_tilesw[ti];
+            e.t_tiles = ctx->has_test ? ctx->t_tilesw[ti].as<int64_t>() : nullptr;
+            e.n_t_tiles = ctx->has_test ? ctx->n_t_tilesw[ti] : 0;
+            e.row_xw = ctx->row_xw.as<double>();
+            launch_eval6(var, e, eval6_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
+            ctx->xw_cached = true;
+        } else
             launch_eval2(eval_version(), e, eval2_blocks(eval_version(), e.n_tiles, e.n_t_tiles), ctx->stream);
     });
     HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));

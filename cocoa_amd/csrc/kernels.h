@@ -194,6 +194,9 @@ int eval2_blocks(int version, int64_t n, int64_t n_test);
 void launch_eval4(int variant, const EvalArgs& a, int blocks, hipStream_t s);
 int eval4_blocks(int variant, int64_t n, int64_t n_test);
 int eval4_tile(int variant);
+void launch_eval6(int variant, const EvalArgs& a, int blocks, hipStream_t s);
+int eval6_blocks(int variant, int64_t n, int64_t n_test);
+int eval6_tile(int variant);
 
 void launch_solver2_fast(int mode, const Solver2Args& a, int grid, size_t lds, hipStream_t s);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);

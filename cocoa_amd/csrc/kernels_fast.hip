@@ -1,6 +1,8 @@
 // Fast translation unit (-ffp-contract=fast): wave-tree dot products and
 // fused multiply-adds.  Results agree with the strict path within the 1e-9
 // relative tolerance of BASELINE.json's north_star.
+#include <cstdlib>
+
 #include "kernels.h"
 #include "solver2_impl.h"
 #include "solver_impl.h"
@@ -494,6 +496,178 @@ void launch_eval4(int variant, const EvalArgs& a, int blocks, hipStream_t s) {
         eval_v4_kernel<4096, 1024, 0><<<blocks, 1024, 0, s>>>(a);
     else
         eval_v4_kernel<2048, 256, 1><<<blocks, 256, 0, s>>>(a);
+    eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+}
+
+// Eval v6: wave tiles.  v4's block-wide tile (stream -> gather -> LDS ->
+// barrier -> row sums -> barrier) keeps a whole 512-thread block in one phase
+// at a time, so a CU's HBM stream stalls while its blocks wait on the w gather.
+// Here every wave owns its own tile of whole rows (<= WT entries, tiles built
+// with cap WT) and its own LDS slice, and the only synchronisation is the
+// in-wave LDS ordering fence: the waves of a CU drift apart and one wave's
+// gather hides behind the others' streams.  PF = 1 also issues the next tile's
+// stream loads before this tile's gathers (register double buffer).
+// Same sums as v4 (OptUtils.scala:65-98 hinge / error, row order inside a
+// 16-lane DPP tree: fast mode).
+template <int WT>
+struct WaveTile {
+    static constexpr int U = WT / 256 + 1;  // 4-entry units per lane (alignment adds one)
+    i32x4 c[U];
+    f64x2 v0[U], v1[U];
+    int64_t r0, r1, e0, e1;
+    bool test;
+};
+
+template <int WT>
+__device__ __forceinline__ void wave_tile_load(const EvalArgs& a, int64_t t, int lane, WaveTile<WT>& x) {
+    x.test = t >= a.n_tiles;
+    const int64_t tt = x.test ? t - a.n_tiles : t;
+    const int64_t* tl = x.test ? a.t_tiles : a.tiles;
+    const int64_t* te = tl + (x.test ? a.n_t_tiles : a.n_tiles) + 1;
+    x.r0 = tl[tt];
+    x.r1 = tl[tt + 1];
+    x.e0 = te[tt];
+    x.e1 = te[tt + 1];
+    const int32_t* cl = x.test ? a.t_col : a.col;
+    const double* vl = x.test ? a.t_val : a.val;
+    const int64_t base = x.e0 & ~(int64_t)3;
+    const int64_t span = (x.e1 - x.e0 > WT) ? 0 : x.e1 - base;  // a long row is streamed separately
+#pragma unroll
+    for (int u = 0; u < WaveTile<WT>::U; ++u) {
+        const int64_t k = 4 * ((int64_t)u * 64 + lane);
+        x.c[u] = i32x4{0, 0, 0, 0};
+        x.v0[u] = f64x2{0.0, 0.0};
+        x.v1[u] = x.v0[u];
+        if (k < span) {
+            x.c[u] = __builtin_nontemporal_load((const i32x4*)(cl + base + k));
+            x.v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
+            x.v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
+        }
+    }
+}
+
+template <int WT, int BLOCK, int PF>
+__global__ __launch_bounds__(BLOCK) void eval_v6_kernel(EvalArgs a) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ double prod_s[NW][WT + 4];
+    __shared__ uint16_t roff_s[NW][WT + 2];
+    __shared__ double red[NW];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double* prod = prod_s[wv];
+    uint16_t* roff = roff_s[wv];
+    const int sub = lane & 15, grp = lane >> 4;
+    double hinge = 0.0, err = 0.0;
+    const int64_t ntiles = a.n_tiles + a.n_t_tiles;
+    const int64_t nwaves = (int64_t)gridDim.x * NW;
+    int64_t t = (int64_t)blockIdx.x * NW + wv;
+    WaveTile<WT> cur, nxt;
+    if (PF && t < ntiles) wave_tile_load<WT>(a, t, lane, cur);
+    for (; t < ntiles; t += nwaves) {
+        if (PF) {
+            if (t + nwaves < ntiles) wave_tile_load<WT>(a, t + nwaves, lane, nxt);
+        } else {
+            wave_tile_load<WT>(a, t, lane, cur);
+        }
+        const bool test = cur.test;
+        const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
+        const double* yy = test ? a.t_y : a.y;
+        const int64_t r0 = cur.r0, e0 = cur.e0, e1 = cur.e1;
+        if (e1 - e0 > WT) {  // one long row: strided stream + wave tree
+            const int32_t* cl = test ? a.t_col : a.col;
+            const double* vl = test ? a.t_val : a.val;
+            double acc = 0.0;
+            for (int64_t q = e0 + lane; q < e1; q += 64) acc += vl[q] * a.w[cl[q]];
+            const double dot = wave_sum(acc);
+            if (lane == 0) {
+                if (!test) {
+                    hinge += jmax(1 - yy[r0] * dot, 0.0);
+                    if (a.row_xw) a.row_xw[r0] = dot;
+                } else {
+                    err += (dot * yy[r0] > 0) ? 0.0 : 1.0;
+                }
+            }
+        } else {
+            const int nr = (int)(cur.r1 - r0);
+            const int64_t base = e0 & ~(int64_t)3;
+            const int sh = (int)(e0 - base);
+            const int64_t span = e1 - base;
+            for (int i = lane; i <= nr; i += 64) roff[i] = (uint16_t)(rp[r0 + i] - e0);
+#pragma unroll
+            for (int u = 0; u < WaveTile<WT>::U; ++u) {
+                const int64_t k = 4 * ((int64_t)u * 64 + lane);
+                if (k < span) {
+                    const double p0 = cur.v0[u].x * a.w[cur.c[u].x];
+                    const double p1 = cur.v0[u].y * a.w[cur.c[u].y];
+                    const double p2 = cur.v1[u].x * a.w[cur.c[u].z];
+                    const double p3 = cur.v1[u].y * a.w[cur.c[u].w];
+                    *(f64x2*)(prod + k) = f64x2{p0, p1};
+                    *(f64x2*)(prod + k + 2) = f64x2{p2, p3};
+                }
+            }
+            wave_lds_sync();
+            for (int r = grp; r < nr; r += 4) {
+                const int b = roff[r] + sh, e = roff[r + 1] + sh;
+                double acc = 0.0;
+                for (int q = b + sub; q < e; q += 16) acc += prod[q];
+                const double dot = row16_sum(acc);
+                if (sub == 0) {
+                    if (!test) {
+                        hinge += jmax(1 - yy[r0 + r] * dot, 0.0);
+                        if (a.row_xw) a.row_xw[r0 + r] = dot;
+                    } else {
+                        err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+                    }
+                }
+            }
+            wave_lds_sync();  // this tile's LDS reads finish before the next tile's writes
+        }
+        if (PF) cur = nxt;
+    }
+    const int64_t gt = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    const int64_t gs = (int64_t)gridDim.x * BLOCK;
+    double al = 0.0, w2 = 0.0;
+    for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
+    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
+    const double s0 = block_sum_n<BLOCK>(hinge, red);
+    const double s1 = block_sum_n<BLOCK>(al, red);
+    const double s2 = block_sum_n<BLOCK>(w2, red);
+    const double s3 = block_sum_n<BLOCK>(err, red);
+    if (threadIdx.x == 0) {
+        double* p = a.partials + (size_t)blockIdx.x * 4;
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+        p[3] = s3;
+    }
+}
+
+// variant: 0 = WT 512 / 256 threads, 1 = WT 512 prefetched, 2 = WT 1024 / 128
+// threads, 3 = WT 256 / 256 threads.  Blocks per CU from the LDS footprint
+// (160 KB per CU) and the 32-wave cap.
+int eval6_tile(int variant) { return variant == 2 ? 1024 : variant == 3 ? 256 : 512; }
+
+int eval6_blocks(int variant, int64_t n_tiles, int64_t n_t_tiles) {
+    const int wt = eval6_tile(variant);
+    const int nw = variant == 2 ? 2 : 4;
+    const int lds = nw * (wt * 10 + 40) + 64;
+    int per_cu = (160 * 1024) / lds;
+    if (per_cu * nw > 32) per_cu = 32 / nw;
+    const char* e = std::getenv("COCOA_EVAL6_PERCU");
+    if (e && std::atoi(e) > 0 && std::atoi(e) < per_cu) per_cu = std::atoi(e);
+    int64_t b = (n_tiles + n_t_tiles + nw - 1) / nw;
+    if (b > 256 * per_cu) b = 256 * per_cu;
+    return (int)(b < 1 ? 1 : b);
+}
+
+void launch_eval6(int variant, const EvalArgs& a, int blocks, hipStream_t s) {
+    if (variant == 1)
+        eval_v6_kernel<512, 256, 1><<<blocks, 256, 0, s>>>(a);
+    else if (variant == 2)
+        eval_v6_kernel<1024, 128, 0><<<blocks, 128, 0, s>>>(a);
+    else if (variant == 3)
+        eval_v6_kernel<256, 256, 0><<<blocks, 256, 0, s>>>(a);
+    else
+        eval_v6_kernel<512, 256, 0><<<blocks, 256, 0, s>>>(a);
     eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
 }
 

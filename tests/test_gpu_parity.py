@@ -317,12 +317,14 @@ def _eval_edge_data(seed=11):
                        np.concatenate([v for _, v in rows]), y, part, d)
 
 
-@pytest.mark.parametrize("version,variant", [("v1", "3"), ("v4", "0"), ("v4", "1"), ("v4", "3")])
+@pytest.mark.parametrize("version,variant", [("v1", "3"), ("v4", "0"), ("v4", "1"), ("v4", "3"),
+                                             ("v6", "0"), ("v6", "1"), ("v6", "2"), ("v6", "3")])
 def test_fast_eval_versions_match_oracle(version, variant, monkeypatch):
     """Every fast eval kernel (OptUtils.scala:57-98) against the oracle on the
     same (w, alpha), including rows longer than a tile and empty rows."""
     monkeypatch.setenv("COCOA_EVAL", version)
     monkeypatch.setenv("COCOA_EVAL4", variant)
+    monkeypatch.setenv("COCOA_EVAL6", variant)
     tr = _eval_edge_data()
     te = tr.row_range(200, 1300)
     od, ot = odata(tr), odata(te)
