@@ -104,6 +104,10 @@ SIGNATURES = {
     "cocoa_set_alpha": (_int, [_vp, _pf64]),
     "cocoa_checkpoint_save": (_int, [_vp, ctypes.c_char_p, _i32]),
     "cocoa_checkpoint_load": (_int, [_vp, ctypes.c_char_p, ctypes.POINTER(_i32)]),
+    "cocoa_set_checkpoint_dir": (_int, [_vp, ctypes.c_char_p]),
+    "cocoa_checkpoint_file": (_int, [_vp, _int, ctypes.c_char_p, _i64]),
+    "cocoa_resume": (_int, [_vp, ctypes.POINTER(Params), ctypes.POINTER(Debug), _int, ctypes.c_char_p, ROUND_CB,
+                            _vp]),
     "cocoa_local_sdca": (_int, [_vp, _i32, _pf64, _i32, _f64, _i32, _pf64, _i32, _int, _f64, _pf64, _pf64]),
     "cocoa_samples": (_int, [_vp, _i32, _i32, _i32, _pi32]),
     "cocoa_stats_enable": (_int, [_vp, _int]),

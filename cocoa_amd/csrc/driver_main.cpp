@@ -181,6 +181,7 @@ int main(int argc, char** argv) {
         check(cocoa_set_train(ctx, K, train.part_ptr, train.row_ptr, train.col, train.val, train.y, train.n_rows,
                               numFeatures, 0, K), ctx);
         if (has_test) check(cocoa_set_test(ctx, test.row_ptr, test.col, test.val, test.y, test.n_rows), ctx);
+        if (!chkptDir.empty()) check(cocoa_set_checkpoint_dir(ctx, chkptDir.c_str()), ctx);  // CoCoA.scala:58-62
         cocoa_params P{n, numRounds, localIters, 0, lambda, beta, gamma};
         cocoa_debug D{debugIter, seed, chkptIter, 0};
 

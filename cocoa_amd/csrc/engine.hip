@@ -87,6 +87,7 @@ struct cocoa_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     std::string err;
+    std::string ckpt_dir;  // cocoa_set_checkpoint_dir: periodic (t, w, alpha) saves in cocoa_run
 
     // training data (this rank)
     int32_t K_loc = 0, K_glob = 0, part_begin = 0, d = 0;
@@ -955,11 +956,15 @@ extern "C" int cocoa_eval_finish(const cocoa_ctx* ctx, double hinge_sum, double 
     return COCOA_OK;
 }
 
-extern "C" int cocoa_run(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
-                         const double* w_init, cocoa_round_cb cb, void* user) {
-    int rc = cocoa_init(ctx, params, debug, method, w_init);
-    if (rc) return rc;
-    for (int32_t t = 1; t <= params->num_rounds; ++t) {
+static std::string checkpoint_path(const cocoa_ctx* ctx, int method = -1);
+
+// Rounds t0+1 .. T of a started run.  With a checkpoint directory set, the
+// (t, w, alpha) state is saved every chkpt_iter rounds, where the reference
+// checkpoints its alpha RDD (CoCoA.scala:58-62; hingeDriver.scala:55-59 turns
+// it off without a chkptDir).
+static int run_rounds(cocoa_ctx* ctx, const cocoa_params* params, int32_t t0, cocoa_round_cb cb, void* user) {
+    int rc = COCOA_OK;
+    for (int32_t t = t0 + 1; t <= params->num_rounds; ++t) {
         rc = cocoa_round(ctx, t);
         if (rc) return rc;
         if (ctx->D.debug_iter > 0 && t % ctx->D.debug_iter == 0) {              // CoCoA.scala:51
@@ -968,8 +973,45 @@ extern "C" int cocoa_run(cocoa_ctx* ctx, const cocoa_params* params, const cocoa
             if (rc) return rc;
             if (cb) cb(user, t, &ev);
         }
+        if (!ctx->ckpt_dir.empty() && ctx->D.chkpt_iter > 0 && t % ctx->D.chkpt_iter == 0) {  // CoCoA.scala:58
+            rc = cocoa_checkpoint_save(ctx, checkpoint_path(ctx).c_str(), t);
+            if (rc) return rc;
+        }
     }
     return cocoa_sync(ctx);
+}
+
+extern "C" int cocoa_run(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
+                         const double* w_init, cocoa_round_cb cb, void* user) {
+    const int rc = cocoa_init(ctx, params, debug, method, w_init);
+    if (rc) return rc;
+    return run_rounds(ctx, params, 0, cb, user);
+}
+
+extern "C" int cocoa_set_checkpoint_dir(cocoa_ctx* ctx, const char* dir) {
+    CAPI_BEGIN(ctx)
+    ctx->ckpt_dir = dir ? dir : "";
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_checkpoint_file(cocoa_ctx* ctx, int method, char* buf, int64_t cap) {
+    CAPI_BEGIN(ctx)
+    require(buf != nullptr && cap > 0, COCOA_E_ARG, "cocoa_checkpoint_file: bad argument");
+    require(!ctx->ckpt_dir.empty(), COCOA_E_STATE, "cocoa_checkpoint_file: no checkpoint directory set");
+    const std::string p = checkpoint_path(ctx, method);
+    require((int64_t)p.size() < cap, COCOA_E_ARG, "cocoa_checkpoint_file: buffer too small");
+    std::memcpy(buf, p.c_str(), p.size() + 1);
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_resume(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
+                            const char* path, cocoa_round_cb cb, void* user) {
+    int rc = cocoa_init(ctx, params, debug, method, nullptr);
+    if (rc) return rc;
+    int32_t t0 = 0;
+    rc = cocoa_checkpoint_load(ctx, path, &t0);
+    if (rc) return rc;
+    return run_rounds(ctx, params, t0, cb, user);
 }
 
 extern "C" int cocoa_sync(cocoa_ctx* ctx) {
@@ -1020,6 +1062,13 @@ extern "C" int cocoa_set_alpha(cocoa_ctx* ctx, const double* alpha_in) {
 }
 
 // ------------------------------------------------------------ checkpoint --
+// <dir>/cocoa_m<method>_p<part_begin>.ck: one file per method and rank, the
+// latest state only (each save replaces the previous one atomically).
+static std::string checkpoint_path(const cocoa_ctx* ctx, int method) {
+    return ctx->ckpt_dir + "/cocoa_m" + std::to_string(method < 0 ? ctx->method : method) + "_p" +
+           std::to_string(ctx->part_begin) + ".ck";
+}
+
 namespace {
 struct CkptHeader {
     char magic[8];

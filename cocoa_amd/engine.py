@@ -76,19 +76,38 @@ class Engine:
         return r.as_dict()
 
     def run(self, method, n, num_rounds, local_iters, lam, beta=1.0, gamma=1.0, debug_iter=10, seed=0,
-            w_init=None, callback=None):
+            w_init=None, callback=None, chkpt_iter=100, resume_from=None):
+        """cocoa_run (or cocoa_resume from a checkpoint file): T rounds with
+        evaluation every debug_iter rounds and, when a checkpoint directory is
+        set, a checkpoint every chkpt_iter rounds (CoCoA.scala:51-62)."""
         self.params = C.Params(n, num_rounds, local_iters, 0, lam, beta, gamma)
-        self.debug = C.Debug(debug_iter, seed, 100, 0)
+        self.debug = C.Debug(debug_iter, seed, chkpt_iter, 0)
 
         def _cb(user, t, ev):
             if callback is not None:
                 callback(t, ev.contents.as_dict())
 
         cb = C.ROUND_CB(_cb)
+        m = C.METHODS[method] if isinstance(method, str) else int(method)
+        if resume_from is not None:
+            assert w_init is None, "a resumed run takes w from the checkpoint"
+            C.check(C.lib().cocoa_resume(self.h, ctypes.byref(self.params), ctypes.byref(self.debug), m,
+                                         os.fsencode(resume_from), cb, None), self.h)
+            return
         wi = None if w_init is None else np.ascontiguousarray(w_init, np.float64)
-        C.check(C.lib().cocoa_run(self.h, ctypes.byref(self.params), ctypes.byref(self.debug),
-                                  C.METHODS[method] if isinstance(method, str) else int(method),
+        C.check(C.lib().cocoa_run(self.h, ctypes.byref(self.params), ctypes.byref(self.debug), m,
                                   C.f64p(wi) if wi is not None else None, cb, None), self.h)
+
+    def set_checkpoint_dir(self, path):
+        """Periodic checkpoints inside run() (None turns them off)."""
+        C.check(C.lib().cocoa_set_checkpoint_dir(self.h, None if path is None else os.fsencode(path)), self.h)
+
+    def checkpoint_file(self, method):
+        """Path of run()'s periodic checkpoint for `method` on this rank."""
+        buf = ctypes.create_string_buffer(4096)
+        m = C.METHODS[method] if isinstance(method, str) else int(method)
+        C.check(C.lib().cocoa_checkpoint_file(self.h, m, buf, len(buf)), self.h)
+        return os.fsdecode(buf.value)
 
     def w(self):
         out = np.zeros(self.d, np.float64)

@@ -64,7 +64,7 @@ typedef struct {
 typedef struct {
     int32_t debug_iter;  /* <= 0: no per-round evaluation                     */
     int32_t seed;        /* round t uses seed + t (CoCoA.scala:45)            */
-    int32_t chkpt_iter;  /* accepted; RDD lineage truncation has no analogue  */
+    int32_t chkpt_iter;  /* rounds between checkpoints (cocoa_set_checkpoint_dir) */
     int32_t _pad;
 } cocoa_debug;
 
@@ -158,6 +158,17 @@ int cocoa_set_alpha(cocoa_ctx *ctx, const double *alpha_in);
  * and alpha, and returns the round t to resume after. */
 int cocoa_checkpoint_save(cocoa_ctx *ctx, const char *path, int32_t t);
 int cocoa_checkpoint_load(cocoa_ctx *ctx, const char *path, int32_t *t_out);
+/* Periodic checkpoints inside cocoa_run / cocoa_resume: with a directory set
+ * (hingeDriver.scala:55-59 chkptDir; NULL or "" turns them off), the state is
+ * saved every debug->chkpt_iter rounds (CoCoA.scala:58-62) to
+ * <dir>/cocoa_m<method>_p<part_begin>.ck, replacing the previous save.
+ * cocoa_checkpoint_file writes that path (NUL-terminated) into buf[cap]. */
+int cocoa_set_checkpoint_dir(cocoa_ctx *ctx, const char *dir);
+int cocoa_checkpoint_file(cocoa_ctx *ctx, int method, char *buf, int64_t cap);
+/* cocoa_run continued from a checkpoint: init, load (t0, w, alpha), then
+ * rounds t0+1 .. num_rounds with the same per-round evaluation and saves. */
+int cocoa_resume(cocoa_ctx *ctx, const cocoa_params *params, const cocoa_debug *debug, int method,
+                 const char *path, cocoa_round_cb cb, void *user);
 
 /* CoCoA.localSDCA (CoCoA.scala:130-192) for ONE partition of the loaded
  * training set, as a unit: w (in/out, mutated when plus == 0, like the

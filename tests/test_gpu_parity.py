@@ -341,6 +341,29 @@ def test_fast_eval_versions_match_oracle(version, variant, monkeypatch):
     assert ev["test_err_count"] == rv["test_err"]
 
 
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd"])
+def test_run_periodic_checkpoint_and_resume(c1, tmp_path, method):
+    """cocoa_run saves (t, w, alpha) every chkptIter rounds (CoCoA.scala:58-62);
+    cocoa_resume from the round-4 save lands bitwise on the uninterrupted
+    6-round run, with the same debug evaluations after the resume point."""
+    tr, te = c1
+    H = max(int(0.1 * tr.n / 4), 1)
+    full, evs = engine(tr, te, strict=True), {}
+    full.run(method, tr.n, 6, H, 1e-3, debug_iter=1, callback=lambda t, ev: evs.__setitem__(t, ev["gap"]))
+    a = engine(tr, te, strict=True)
+    a.set_checkpoint_dir(str(tmp_path))
+    a.run(method, tr.n, 5, H, 1e-3, debug_iter=0, chkpt_iter=2)  # saves at t = 2, 4
+    path = a.checkpoint_file(method)
+    assert os.path.exists(path)
+    b, evb = engine(tr, te, strict=True), {}
+    b.run(method, tr.n, 6, H, 1e-3, debug_iter=1, resume_from=path,
+          callback=lambda t, ev: evb.__setitem__(t, ev["gap"]))
+    assert sorted(evb) == [5, 6]
+    assert evb == {t: evs[t] for t in (5, 6)}
+    assert np.array_equal(full.w(), b.w())
+    assert np.array_equal(full.alpha(), b.alpha())
+
+
 @pytest.mark.parametrize("method", ["mbsgd", "localsgd"])
 def test_c2_fast_sgd_matches_strict(c2, method):
     """Full-size C5 check: the fast SGD kernels (parallel mb-SGD steps, local
