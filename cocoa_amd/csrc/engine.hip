@@ -924,7 +924,7 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
                 e.t_tiles = ctx->has_test ? ctx->t_tiles4k.as<int64_t>() : nullptr;
                 e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles4k : 0;
             }
-            const bool exact = var == 0 || var == 1 || var == 3 || var == 8;  // the rest are timing diagnostics
+            const bool exact = var == 0 || var == 1 || var == 3 || var == 8 || var == 12 || var == 13;  // the rest are timing diagnostics
             e.row_xw = exact ? ctx->row_xw.as<double>() : nullptr;
             launch_eval4(var, e, eval4_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
             ctx->xw_cached = exact;  // the next round's plan reuses these x.w (stream order)

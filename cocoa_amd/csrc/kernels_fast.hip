@@ -360,6 +360,7 @@ __global__ __launch_bounds__(BLOCK) void eval_v4_kernel(EvalArgs a) {
         if (GATHER == 2) return (c & 7) == 0 ? v * a.w[c] : v;
         if (GATHER == 3) return v * wl[c & 2047];
         if (GATHER == 5) return v * a.w[c & 2047];
+        if (GATHER == 6) return v * a.w[c >> 31];  // every lane reads w[0]: one line per instruction
         return v;
     };
     __shared__ uint16_t roff[TILE + 2];
@@ -461,13 +462,137 @@ __global__ __launch_bounds__(BLOCK) void eval_v4_kernel(EvalArgs a) {
     }
 }
 
+// Eval v7: v4 with the per-tile dependent round trips taken off the critical
+// path.  v4 waits on row_ptr before it issues the tile's stream (its roff loop
+// comes first), reads y only after each row's dot, and reads the tile bounds
+// only when the tile starts: up to five serialized memory latencies per tile.
+// Here the next tile's bounds are read one tile ahead, the row_ptr and y
+// values go to registers in the same batch as the stream, and LDS is written
+// only after the batch lands.  Same arithmetic as v4.
+template <int TILE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void eval_v7_kernel(EvalArgs a) {
+    constexpr int UNITS = TILE / (4 * BLOCK);
+    __shared__ double prod[TILE + 4];
+    __shared__ uint16_t roff[TILE + 2];
+    __shared__ double ys[BLOCK];  // y of the tile's first BLOCK rows
+    __shared__ double red[BLOCK / 64];
+    const int tid = threadIdx.x;
+    const int sub = tid & 15, grp = tid >> 4;
+    double hinge = 0.0, err = 0.0;
+    const int64_t ntiles = a.n_tiles + a.n_t_tiles;
+    auto bounds = [&](int64_t t, int64_t& r0, int64_t& r1, int64_t& e0, int64_t& e1) {
+        const bool test = t >= a.n_tiles;
+        const int64_t tt = test ? t - a.n_tiles : t;
+        const int64_t* tl = test ? a.t_tiles : a.tiles;
+        const int64_t* te = tl + (test ? a.n_t_tiles : a.n_tiles) + 1;
+        r0 = tl[tt];
+        r1 = tl[tt + 1];
+        e0 = te[tt];
+        e1 = te[tt + 1];
+    };
+    int64_t nr0 = 0, nr1 = 0, ne0 = 0, ne1 = 0;
+    if ((int64_t)blockIdx.x < ntiles) bounds(blockIdx.x, nr0, nr1, ne0, ne1);
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t r0 = nr0, r1 = nr1, e0 = ne0, e1 = ne1;
+        if (t + gridDim.x < ntiles) bounds(t + gridDim.x, nr0, nr1, ne0, ne1);
+        const bool test = t >= a.n_tiles;
+        const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
+        const int32_t* cl = test ? a.t_col : a.col;
+        const double* vl = test ? a.t_val : a.val;
+        const double* yy = test ? a.t_y : a.y;
+        const int64_t T = e1 - e0;
+        if (T > TILE) {
+            double acc = 0.0;
+            for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += vl[q] * a.w[cl[q]];
+            const double dot = block_sum_n<BLOCK>(acc, red);
+            if (tid == 0) {
+                if (!test) {
+                    hinge += jmax(1 - yy[r0] * dot, 0.0);
+                    if (a.row_xw) a.row_xw[r0] = dot;
+                } else {
+                    err += (dot * yy[r0] > 0) ? 0.0 : 1.0;
+                }
+            }
+            continue;
+        }
+        const int nr = (int)(r1 - r0);
+        const int64_t base = e0 & ~(int64_t)3;
+        const int sh = (int)(e0 - base);
+        const int64_t span = e1 - base;
+        i32x4 c[UNITS + 1];
+        f64x2 v0[UNITS + 1], v1[UNITS + 1];
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            c[u] = i32x4{0, 0, 0, 0};
+            v0[u] = f64x2{0.0, 0.0};
+            v1[u] = v0[u];
+            if (k < span) {
+                c[u] = __builtin_nontemporal_load((const i32x4*)(cl + base + k));
+                v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
+                v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
+            }
+        }
+        const int64_t rpv = tid <= nr ? rp[r0 + tid] : 0;  // same batch as the stream
+        const double yv = tid < nr ? yy[r0 + tid] : 0.0;
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            if (k < span) {
+                const double p0 = v0[u].x * a.w[c[u].x];
+                const double p1 = v0[u].y * a.w[c[u].y];
+                const double p2 = v1[u].x * a.w[c[u].z];
+                const double p3 = v1[u].y * a.w[c[u].w];
+                *(f64x2*)(prod + k) = f64x2{p0, p1};
+                *(f64x2*)(prod + k + 2) = f64x2{p2, p3};
+            }
+        }
+        if (tid <= nr) roff[tid] = (uint16_t)(rpv - e0);
+        if (tid < nr) ys[tid] = yv;
+        for (int i = tid + BLOCK; i <= nr; i += BLOCK) roff[i] = (uint16_t)(rp[r0 + i] - e0);  // tiles of tiny rows
+        __syncthreads();
+        for (int r = grp; r < nr; r += BLOCK / 16) {
+            const int b = roff[r] + sh, e = roff[r + 1] + sh;
+            double acc = 0.0;
+            for (int q = b + sub; q < e; q += 16) acc += prod[q];
+            const double dot = row16_sum(acc);
+            if (sub == 0) {
+                const double yr = r < BLOCK ? ys[r] : yy[r0 + r];
+                if (!test) {
+                    hinge += jmax(1 - yr * dot, 0.0);
+                    if (a.row_xw) a.row_xw[r0 + r] = dot;
+                } else {
+                    err += (dot * yr > 0) ? 0.0 : 1.0;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t gt = (int64_t)blockIdx.x * BLOCK + tid;
+    const int64_t gs = (int64_t)gridDim.x * BLOCK;
+    double al = 0.0, w2 = 0.0;
+    for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
+    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
+    const double s0 = block_sum_n<BLOCK>(hinge, red);
+    const double s1 = block_sum_n<BLOCK>(al, red);
+    const double s2 = block_sum_n<BLOCK>(w2, red);
+    const double s3 = block_sum_n<BLOCK>(err, red);
+    if (tid == 0) {
+        double* p = a.partials + (size_t)blockIdx.x * 4;
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+        p[3] = s3;
+    }
+}
+
 int eval4_tile(int variant) { return variant == 1 || variant == 3 || variant >= 4 ? 4096 : 2048; }
 
 // variant: 0 = tile 2048 / 8 blocks per CU, 1 = tile 4096 / 4 per CU,
 //          2 = tile 2048 without the w gather (diagnostic: stream-only time),
 //          3 = tile 4096 / 4 per CU, 512 threads
 int eval4_blocks(int variant, int64_t n_tiles, int64_t n_t_tiles) {
-    const int per_cu = variant >= 8 ? 2 : (variant == 1 || variant >= 3 ? 3 : 7);  // LDS: 41 KB / 20.5 KB per block
+    const int per_cu = (variant >= 8 && variant <= 10) ? 2 : (variant == 1 || variant >= 3 ? 3 : 7);  // LDS: 41 KB / 20.5 KB per block
     int64_t b = n_tiles + n_t_tiles;
     if (b > 256 * per_cu) b = 256 * per_cu;
     return (int)(b < 1 ? 1 : b);
@@ -494,6 +619,12 @@ void launch_eval4(int variant, const EvalArgs& a, int blocks, hipStream_t s) {
         eval_v4_kernel<4096, 1024, 5><<<blocks, 1024, 0, s>>>(a);
     else if (variant == 10)
         eval_v4_kernel<4096, 1024, 0><<<blocks, 1024, 0, s>>>(a);
+    else if (variant == 11)
+        eval_v4_kernel<4096, 512, 6><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 12)
+        eval_v7_kernel<4096, 512><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 13)
+        eval_v7_kernel<4096, 256><<<blocks, 256, 0, s>>>(a);
     else
         eval_v4_kernel<2048, 256, 1><<<blocks, 256, 0, s>>>(a);
     eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
