@@ -87,7 +87,17 @@ struct cocoa_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     std::string err;
-    std::string ckpt_dir;  // cocoa_set_checkpoint_dir: periodic (t, w, alpha) saves in cocoa_run
+    std::string ckpt_dir;
+    // Double-buffered deltaW slices (large K_loc * d, e.g. C4): round t works in
+    // set t & 1; the set round t folded is re-zeroed by a memset on zstream
+    // that starts with round t+1 (after round t's eval, so the bandwidth-bound
+    // eval does not share HBM with it) and runs beside the latency-bound solver.
+    DevBuf dw2;
+    bool dw_dbuf = false;
+    hipStream_t zstream = nullptr;
+    hipEvent_t zdone[2] = {nullptr, nullptr}, folded = nullptr;
+    bool zpending[2] = {false, false};
+    int zero_owed = -1;  // set folded last round, re-zeroed once the next round starts  // cocoa_set_checkpoint_dir: periodic (t, w, alpha) saves in cocoa_run
 
     // training data (this rank)
     int32_t K_loc = 0, K_glob = 0, part_begin = 0, d = 0;
@@ -194,6 +204,12 @@ struct cocoa_ctx {
     }
     ~cocoa_ctx() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (zstream) {
+            (void)hipStreamSynchronize(zstream);
+            (void)hipStreamDestroy(zstream);
+            for (auto e : zdone) (void)hipEventDestroy(e);
+            (void)hipEventDestroy(folded);
+        }
         for (auto& p : pending) {
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
@@ -614,6 +630,8 @@ static bool v2_enabled() {
     return e && std::strcmp(e, "v2") == 0;
 }
 
+static bool dw_double_buffer(size_t bytes);
+
 extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
                           const double* w_init) {
     CAPI_BEGIN(ctx)
@@ -649,7 +667,21 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         HIPCHK(hipMemsetAsync(ctx->w.p, 0, sizeof(double) * (size_t)d, s));
     ctx->alpha.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
     ctx->alpha_work.alloc(sizeof(double) * (size_t)std::max<int64_t>(n, 1));
+    if (ctx->zstream) HIPCHK(hipStreamSynchronize(ctx->zstream));  // no re-zeroing in flight
+    ctx->zpending[0] = ctx->zpending[1] = false;
+    ctx->zero_owed = -1;
     ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * d), s);
+    ctx->dw_dbuf = dw_double_buffer((size_t)(K * d) * sizeof(double));
+    if (ctx->dw_dbuf) {
+        ctx->dw2.alloc_zero(sizeof(double) * (size_t)(K * d), s);
+        if (!ctx->zstream) {
+            HIPCHK(hipStreamCreateWithFlags(&ctx->zstream, hipStreamNonBlocking));
+            for (auto& e : ctx->zdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ctx->folded, hipEventDisableTiming));
+        }
+    } else {
+        ctx->dw2.free();
+    }
     const bool need_wloc = method == COCOA_METHOD_COCOA || method == COCOA_METHOD_LOCALSGD;
     ctx->method = method;
     plan_solver(ctx);
@@ -748,6 +780,15 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     CAPI_END(ctx)
 }
 
+// Double-buffer the deltaW slices when a dense fold's zeroing pass is large:
+// K_loc * d * 8 >= 1 GiB (C4: 1,024 x 3.23 M doubles = 26.5 GB per set).
+// COCOA_DW_DBUF=0 / 1 forces it off / on.
+static bool dw_double_buffer(size_t bytes) {
+    const char* e = std::getenv("COCOA_DW_DBUF");
+    if (e) return std::atoi(e) != 0;
+    return bytes >= ((size_t)1 << 30);
+}
+
 static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
     require(c->inited, COCOA_E_STATE, "cocoa_round: call cocoa_init first");
     const int32_t H = c->P.local_iters;
@@ -756,6 +797,28 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
     const int64_t d = c->d;
     const int K = c->K_loc;
     c->mult = c->scaling;
+    const int set = c->dw_dbuf ? (t & 1) : 0;
+    double* dws = set ? c->dw2.as<double>() : c->dw.as<double>();
+    if (c->zpending[set]) {  // this set's re-zeroing (two rounds ago) must land first
+        HIPCHK(hipStreamWaitEvent(s, c->zdone[set], 0));
+        c->zpending[set] = false;
+    }
+    c->sa.dw = dws;
+    c->sa2.dw = dws;
+    if (c->zero_owed >= 0) {
+        double* zs = c->zero_owed ? c->dw2.as<double>() : c->dw.as<double>();
+        HIPCHK(hipEventRecord(c->folded, s));
+        HIPCHK(hipStreamWaitEvent(c->zstream, c->folded, 0));
+        const char* zb = std::getenv("COCOA_ZERO_WGS");
+        const int blocks = zb ? std::atoi(zb) : 0;  // 0: hipMemsetAsync (C4: 22.8-23.3 ms/round; 64-128 WGs of zero_kernel: 23.0)
+        if (blocks > 0)
+            launch_zero(zs, (int64_t)K * d, blocks, c->zstream);
+        else
+            HIPCHK(hipMemsetAsync(zs, 0, sizeof(double) * (size_t)K * (size_t)d, c->zstream));
+        HIPCHK(hipEventRecord(c->zdone[c->zero_owed], c->zstream));
+        c->zpending[c->zero_owed] = true;
+        c->zero_owed = -1;
+    }
     if (H >= 1) {
         c->timed(COCOA_K_SAMPLE, [&] {
             launch_sampler(c->part_ptr.as<int64_t>(), K, seed, H, c->samples.as<int32_t>(), c->jump.as<uint64_t>(), s);
@@ -822,9 +885,10 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         c->mult = step * c->scaling;
     }
     c->timed(COCOA_K_FOLD, [&] {
-        launch_fold(c->dw.as<double>(), K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply,
-                    c->d_inv.as<int32_t>(), s);
+        launch_fold(dws, K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, c->d_inv.as<int32_t>(),
+                    !c->dw_dbuf, s);
     });
+    if (c->dw_dbuf) c->zero_owed = set;
     c->xw_cached = false;  // w moves this round (scale / fused apply / the caller's apply)
 }
 
@@ -1245,7 +1309,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
             launch_solver_fast(plus ? MODE_PLUS : MODE_COCOA, c.vec_lds, c.alpha_lds, a, 1, c.lds_bytes, s);
         HIPCHK(hipGetLastError());
     }
-    launch_fold(dwb.as<double>(), 1, d, sumb.as<double>(), nullptr, 1.0, false, ctx->d_inv.as<int32_t>(), s);
+    launch_fold(dwb.as<double>(), 1, d, sumb.as<double>(), nullptr, 1.0, false, ctx->d_inv.as<int32_t>(), true, s);
     HIPCHK(hipGetLastError());
     std::vector<double> old(alpha, alpha + nl);
     HIPCHK(hipMemcpyAsync(delta_w, sumb.p, sizeof(double) * (size_t)d, hipMemcpyDeviceToHost, s));

@@ -71,14 +71,14 @@ void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H,
 // round; then w += sum * mult (CoCoA.scala:48) or the sum is stored for an
 // external all-reduce.
 __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_t d, double* dw_sum, double* w,
-                                                   double mult, int apply, const int32_t* inv) {
+                                                   double mult, int apply, const int32_t* inv, int zero) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
         double s = dw[j];
-        dw[j] = 0.0;
+        if (zero) dw[j] = 0.0;
         for (int32_t k = 1; k < K; ++k) {
             const size_t o = (size_t)k * d + j;
             s = s + dw[o];
-            dw[o] = 0.0;
+            if (zero) dw[o] = 0.0;
         }
         if (apply)
             w[j] = w[j] + (s * mult);
@@ -88,10 +88,26 @@ __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_
 }
 
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
-                 const int32_t* inv, hipStream_t s) {
+                 const int32_t* inv, bool zero, hipStream_t s) {
     int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
     if (blocks < 1) blocks = 1;
-    fold_kernel<<<blocks, 256, 0, s>>>(const_cast<double*>(dw), K, d, dw_sum, w, mult, apply ? 1 : 0, inv);
+    fold_kernel<<<blocks, 256, 0, s>>>(const_cast<double*>(dw), K, d, dw_sum, w, mult, apply ? 1 : 0, inv, zero ? 1 : 0);
+}
+
+// Background re-zeroing of a folded deltaW set (double-buffered slices): a
+// narrow grid of 16-byte non-temporal stores, so it drains at a bounded rate
+// beside the latency-bound local solver instead of competing for all of HBM.
+__global__ __launch_bounds__(256) void zero_kernel(double* p, int64_t n2) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    f64x2* q = (f64x2*)p;
+    const f64x2 z = {0.0, 0.0};
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256)
+        __builtin_nontemporal_store(z, q + i);
+}
+
+void launch_zero(double* p, int64_t n, int blocks, hipStream_t s) {
+    if (n & 1) (void)hipMemsetAsync(p + n - 1, 0, sizeof(double), s);
+    if (n >= 2) zero_kernel<<<blocks < 1 ? 1 : blocks, 256, 0, s>>>(p, n / 2);
 }
 
 __global__ __launch_bounds__(256) void apply_kernel(double* w, const double* dw_sum, int64_t d, double mult,

@@ -342,6 +342,26 @@ def test_fast_eval_versions_match_oracle(version, variant, monkeypatch):
     assert ev["test_err_count"] == rv["test_err"]
 
 
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"])
+def test_double_buffered_deltaw_is_bitwise(c1, method, monkeypatch):
+    """Double-buffered deltaW slices (set t & 1, the folded set re-zeroed by a
+    memset on a side stream; on by default only for K_loc*d >= 1 GiB, i.e. C4)
+    give the single-buffer run's w and alpha bit for bit."""
+    tr, te = c1
+    H = max(int(0.1 * tr.n / 4), 1)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("COCOA_DW_DBUF", flag)
+        e = engine(tr, te, strict=True)
+        e.init(method, tr.n, 5, H, 1e-3)
+        for t in range(1, 6):
+            e.round(t)
+        out.append((e.w(), e.alpha(), e.eval()["primal"]))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2]
+
+
 @pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd"])
 def test_run_periodic_checkpoint_and_resume(c1, tmp_path, method):
     """cocoa_run saves (t, w, alpha) every chkptIter rounds (CoCoA.scala:58-62);
