@@ -612,6 +612,17 @@ static int eval_version() {
 // v2 is opt-in (COCOA_SOLVER=v2): on C2 it measured 10.5 ms/round against
 // v1's 9.8 ms (profiles/r01_bench_v2.json), so v1 stays the default.
 // fast CoCoA+/MbCD step chain: v3 (pipelined, branch-free) unless COCOA_CHAIN=v1
+// Register chunks of chain v3 (rows with z <= 64 * chunks keep their entries in
+// registers).  Measured on MI355X (r01, profiles/r01/regchunks/): 3 chunks
+// against 4 is -6% per round on C5 MbCD (mean row 75.6), neutral on C2 CoCoA+
+// (+0.1% in a same-box A/B) and +2% on C4 CoCoA+ (mean 116).  So MbCD on short
+// rows takes 3, everything else 4; COCOA_REG_CHUNKS_RT = 3 / 4 forces one.
+static int reg_chunks_for(int64_t nnz, int64_t rows, int method) {
+    const char* e = std::getenv("COCOA_REG_CHUNKS_RT");
+    if (e && (std::atoi(e) == 3 || std::atoi(e) == kRegChunks)) return std::atoi(e);
+    return (method == COCOA_METHOD_MBCD && kRegChunks >= 3 && rows > 0 && nnz <= 96 * rows) ? 3 : kRegChunks;
+}
+
 static int chain_version() {
     const char* e = std::getenv("COCOA_CHAIN");
     return (e && std::strcmp(e, "v1") == 0) ? 1 : 3;
@@ -716,6 +727,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 0;
     a.chain = chain_version();
+    a.reg_chunks = reg_chunks_for(ctx->tr.nnz, ctx->tr.n, ctx->method);
     a.prof = nullptr;
     a.lam_n = params->lambda * (double)params->n;
     a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
@@ -1297,6 +1309,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 1;
     a.chain = chain_version();
+    a.reg_chunks = reg_chunks_for(ctx->tr.nnz, ctx->tr.n, ctx->method);
     a.prof = nullptr;
     a.lam_n = lambda * (double)n;
     a.sigma = sigma;

@@ -14,7 +14,10 @@ enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2 };
 
 constexpr int kWave = 64;
 constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
-constexpr int kRegChunks = 4;       // rows with z <= 256 keep (col,val,vec) in registers
+#ifndef COCOA_REG_CHUNKS
+#define COCOA_REG_CHUNKS 4
+#endif
+constexpr int kRegChunks = COCOA_REG_CHUNKS;  // rows with z <= 64 * kRegChunks keep (col,val,vec) in registers
 constexpr int kEvalTile = 2048;     // entries (and max rows) per fast-eval tile
 
 // Per-batch step metadata, staged by the loader wave in LDS (SoA).
@@ -60,7 +63,7 @@ struct SolverArgs {
     int32_t any_dup;
     int32_t raw_alpha;        // 1: write the raw local alpha (unit localSDCA API)
     int32_t chain;            // fast CoCoA+/MbCD: 3 = pipelined branch-free step chain, 1 = v1 chain
-    int32_t pad0;
+    int32_t reg_chunks;       // chain v3: register chunks per row, 3 or kRegChunks (engine: reg_chunks_for)
     double lam_n;             // lambda * n
     double sigma;             // sigma' = K * gamma (CoCoA+)
     double scaling;           // alpha <- alphaOld + dAlpha * scaling

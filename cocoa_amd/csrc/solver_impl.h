@@ -386,9 +386,10 @@ __device__ void compute_batch(const SolverArgs& a, const BatchMeta* mb, const in
 //     the finite values reachable here; +-0 and NaN differ only in the sign of
 //     zero), and a skipped step (projected gradient 0) is coef = 0, na = aa.
 // Agrees with the strict path within the north_star tolerance (fast mode).
+template <int RC>
 struct Chunks3 {
-    int32_t c[kRegChunks];
-    double v[kRegChunks];
+    int32_t c[RC];
+    double v[RC];
 };
 
 struct Meta3 {
@@ -415,12 +416,13 @@ __device__ __forceinline__ Meta3 read_meta3(const BatchMeta* mb, int s, const do
 
 // (col, val) of a staged row, branch-free: lanes past z read the row's last
 // entry (a valid column) with value 0.
-__device__ __forceinline__ void read_chunks3(const int32_t* scol, const double* sval, const Meta3& m, Chunks3& ch) {
+template <int RC>
+__device__ __forceinline__ void read_chunks3(const int32_t* scol, const double* sval, const Meta3& m, Chunks3<RC>& ch) {
     const int lane = lane_id();
     const bool ok = m.off >= 0 && m.z > 0;
     const int32_t last = ok ? m.off + m.z - 1 : 0;
 #pragma unroll
-    for (int u = 0; u < kRegChunks; ++u) {
+    for (int u = 0; u < RC; ++u) {
         const int32_t p = lane + 64 * u;
         const int32_t q = min(m.off + p, last);
         ch.c[u] = scol[q];
@@ -429,7 +431,9 @@ __device__ __forceinline__ void read_chunks3(const int32_t* scol, const double* 
     }
 }
 
-template <int MODE, bool VEC_LDS>
+// RC: register chunks per row (rows with z <= 64 * RC take the register path);
+// SolverArgs::reg_chunks picks 3 or 4 from the data's mean row length.
+template <int MODE, bool VEC_LDS, int RC>
 __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const int32_t* scol, const double* sval,
                                double* vec, double* alv) {
     const int lane = lane_id();
@@ -438,7 +442,7 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
     const double inv_lam_n = 1.0 / a.lam_n;
     const double sigma = a.sigma;
     Meta3 nm = read_meta3(mb, 0, alv);
-    Chunks3 nc;
+    Chunks3<RC> nc;
     read_chunks3(scol, sval, nm, nc);
     // CoCoA.scala:159-186 / MinibatchCD.scala:104-123, branch-free
     auto rule = [&](const Meta3& st, double sdot, double& na, double& coef) -> bool {
@@ -460,26 +464,26 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
     };
     for (int s = 0; s < m; ++s) {
         const Meta3 st = nm;
-        const Chunks3 ch = nc;
+        const Chunks3<RC> ch = nc;
         const int nch = (st.z + 63) >> 6;
-        const bool regs = st.off >= 0 && nch <= kRegChunks && (st.fl & 1) == 0;
+        const bool regs = st.off >= 0 && nch <= RC && (st.fl & 1) == 0;
         double na, coef;
         if (MODE == MODE_PLUS && regs) {
             // CoCoA+ register path, one uniform branch per step: the dependent
             // gather goes out first (chunks past z hit the row's last column,
             // v = 0), then the next step's staged inputs
-            double pd[kRegChunks];
+            double pd[RC];
 #pragma unroll
-            for (int u = 0; u < kRegChunks; ++u) pd[u] = vec[ch.c[u]];
+            for (int u = 0; u < RC; ++u) pd[u] = vec[ch.c[u]];
             next(s);
             double acc = 0.0;
 #pragma unroll
-            for (int u = 0; u < kRegChunks; ++u) acc = fma(ch.v[u], pd[u], acc);
+            for (int u = 0; u < RC; ++u) acc = fma(ch.v[u], pd[u], acc);
             const bool go = rule(st, wave_sum(acc), na, coef);
             if (s + 1 < m && nm.r == st.r) nm.aa = na;           // same row sampled twice in a row
             if (uni((int32_t)go)) {
 #pragma unroll
-                for (int u = 0; u < kRegChunks; ++u)
+                for (int u = 0; u < RC; ++u)
                     if (u < nch && lane + 64 * u < st.z) vec[ch.c[u]] = fma(ch.v[u], coef, pd[u]);  // deltaW += update
                 if (lane == 0) alv[st.r] = na;                   // CoCoA.scala:186
             }
@@ -514,7 +518,7 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
             if (regs) {
                 // MbCD register path: atomic adds into deltaW
 #pragma unroll
-                for (int u = 0; u < kRegChunks; ++u) {
+                for (int u = 0; u < RC; ++u) {
                     if (u < nch && lane + 64 * u < st.z) {
                         if (VEC_LDS)
                             atomicAdd(vec + ch.c[u], ch.v[u] * coef);
@@ -552,7 +556,9 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
     }
 }
 
-template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS>
+// RC: chain v3 register chunks, a separate instantiation per count (one kernel
+// holding both paths measured slower: its register allocation covers both).
+template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS, int RC = kRegChunks>
 __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int k = blockIdx.x;
@@ -595,8 +601,8 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
                                      (int32_t*)(lds + a.lds_stream_col[cur ^ 1]), (double*)(lds + a.lds_stream_val[cur ^ 1]),
                                      prod);
         } else if (!STRICT && MODE != MODE_COCOA && a.chain == 3) {
-            compute_batch3<MODE, VEC_LDS>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
-                                          (const double*)(lds + a.lds_stream_val[cur]), vec, alv);
+            compute_batch3<MODE, VEC_LDS, RC>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
+                                              (const double*)(lds + a.lds_stream_val[cur]), vec, alv);
         } else {
             compute_batch<MODE, STRICT, VEC_LDS, ALPHA_LDS>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
                                                             (const double*)(lds + a.lds_stream_val[cur]), scratch, vec,
@@ -639,7 +645,8 @@ void launch_solver_impl(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
                         hipStream_t s) {
 #define COCOA_LAUNCH(M, V, A)                                                                        \
     do {                                                                                             \
-        auto kern = solver_kernel<M, STRICT, V, A>;                                                  \
+        constexpr int RC3 = (STRICT || M == MODE_COCOA) ? kRegChunks : 3;                         \
+        auto kern = a.reg_chunks == 3 ? solver_kernel<M, STRICT, V, A, RC3> : solver_kernel<M, STRICT, V, A>; \
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
         kern<<<grid, 128, lds, s>>>(a);                                                              \
     } while (0)
