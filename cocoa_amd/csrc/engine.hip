@@ -613,14 +613,18 @@ static int eval_version() {
 // v1's 9.8 ms (profiles/r01_bench_v2.json), so v1 stays the default.
 // fast CoCoA+/MbCD step chain: v3 (pipelined, branch-free) unless COCOA_CHAIN=v1
 // Register chunks of chain v3 (rows with z <= 64 * chunks keep their entries in
-// registers).  Measured on MI355X (r01, profiles/r01/regchunks/): 3 chunks
-// against 4 is -6% per round on C5 MbCD (mean row 75.6), neutral on C2 CoCoA+
-// (+0.1% in a same-box A/B) and +2% on C4 CoCoA+ (mean 116).  So MbCD on short
-// rows takes 3, everything else 4; COCOA_REG_CHUNKS_RT = 3 / 4 forces one.
+// registers).  Measured on MI355X (r01, profiles/r01/regchunks/), C5 MbCD
+// (mean row 75.6): 6.73 ms per round with 4 chunks, 6.34 with 3, 6.09 with 2;
+// C2 CoCoA+: 3 is neutral (+0.1% in a same-box A/B), 2 is +0.7%; C4 CoCoA+
+// (mean 116): 3 is +2%.  So MbCD on short rows takes short_row_chunks (2) and
+// everything else kRegChunks.  COCOA_REG_CHUNKS_RT = short / full forces one.
 static int reg_chunks_for(int64_t nnz, int64_t rows, int method) {
+    const int mode = method == COCOA_METHOD_MBCD ? MODE_MBCD : method == COCOA_METHOD_COCOA ? MODE_COCOA : MODE_PLUS;
+    const int short_rc = short_row_chunks(mode, false);
     const char* e = std::getenv("COCOA_REG_CHUNKS_RT");
-    if (e && (std::atoi(e) == 3 || std::atoi(e) == kRegChunks)) return std::atoi(e);
-    return (method == COCOA_METHOD_MBCD && kRegChunks >= 3 && rows > 0 && nnz <= 96 * rows) ? 3 : kRegChunks;
+    if (e && std::strcmp(e, "short") == 0) return short_rc;
+    if (e && std::strcmp(e, "full") == 0) return kRegChunks;
+    return (mode == MODE_MBCD && rows > 0 && nnz <= 96 * rows) ? short_rc : kRegChunks;
 }
 
 static int chain_version() {

@@ -18,6 +18,11 @@ constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader la
 #define COCOA_REG_CHUNKS 4
 #endif
 constexpr int kRegChunks = COCOA_REG_CHUNKS;  // rows with z <= 64 * kRegChunks keep (col,val,vec) in registers
+// Chain v3's short-row register-chunk count per mode (the engine picks it for
+// data with short rows): MbCD 2, CoCoA+ 3; strict and CoCoA have no variant.
+constexpr int short_row_chunks(int mode, bool strict) {
+    return (strict || mode == 1) ? kRegChunks : (mode == 2 ? (kRegChunks < 2 ? kRegChunks : 2) : (kRegChunks < 3 ? kRegChunks : 3));
+}
 constexpr int kEvalTile = 2048;     // entries (and max rows) per fast-eval tile
 
 // Per-batch step metadata, staged by the loader wave in LDS (SoA).
@@ -63,7 +68,7 @@ struct SolverArgs {
     int32_t any_dup;
     int32_t raw_alpha;        // 1: write the raw local alpha (unit localSDCA API)
     int32_t chain;            // fast CoCoA+/MbCD: 3 = pipelined branch-free step chain, 1 = v1 chain
-    int32_t reg_chunks;       // chain v3: register chunks per row, 3 or kRegChunks (engine: reg_chunks_for)
+    int32_t reg_chunks;       // chain v3: register chunks per row, kRegChunks or short_row_chunks() (engine: reg_chunks_for)
     double lam_n;             // lambda * n
     double sigma;             // sigma' = K * gamma (CoCoA+)
     double scaling;           // alpha <- alphaOld + dAlpha * scaling

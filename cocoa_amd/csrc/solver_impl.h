@@ -645,8 +645,8 @@ void launch_solver_impl(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
                         hipStream_t s) {
 #define COCOA_LAUNCH(M, V, A)                                                                        \
     do {                                                                                             \
-        constexpr int RC3 = (STRICT || M == MODE_COCOA) ? kRegChunks : 3;                         \
-        auto kern = a.reg_chunks == 3 ? solver_kernel<M, STRICT, V, A, RC3> : solver_kernel<M, STRICT, V, A>; \
+        constexpr int RCS = short_row_chunks(M, STRICT);                                           \
+        auto kern = a.reg_chunks == RCS ? solver_kernel<M, STRICT, V, A, RCS> : solver_kernel<M, STRICT, V, A>; \
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
         kern<<<grid, 128, lds, s>>>(a);                                                              \
     } while (0)

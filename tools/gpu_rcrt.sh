@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 T="python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread"
 timeout -k 10 300 $T > gpurun_out/rcrt_tests.log 2>&1 || { tail -20 gpurun_out/rcrt_tests.log; exit 1; }
 tail -1 gpurun_out/rcrt_tests.log
-timeout -k 10 300 env COCOA_REG_CHUNKS_RT=3 $T > gpurun_out/rcrt_tests4.log 2>&1 || { tail -20 gpurun_out/rcrt_tests4.log; exit 1; }
+timeout -k 10 300 env COCOA_REG_CHUNKS_RT=short $T > gpurun_out/rcrt_tests4.log 2>&1 || { tail -20 gpurun_out/rcrt_tests4.log; exit 1; }
 tail -1 gpurun_out/rcrt_tests4.log
 for args in "--steps 20 --warmup 3" "--method mbcd --steps 5 --warmup 2" "--config c4 --steps 5 --warmup 2"; do
   tag=$(echo $args | cut -d' ' -f1-2 | tr -d ' -')
