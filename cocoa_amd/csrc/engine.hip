@@ -997,6 +997,9 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
             launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
         else if (eval_version() == 4) {
             const char* ev = std::getenv("COCOA_EVAL4");
+            // 3 (nontemporal stream) stays the default: plain loads (18) make the pass
+            // 7% faster (0.210 vs 0.227 ms on C2) but leave the CSR in L2/MALL, and
+            // the next round's solver then runs 0.06 ms slower (profiles/r01/evalab/)
             const int var = ev ? std::atoi(ev) : 3;
             if (eval4_tile(var) == 4096) {  // v4 variant tiles
                 e.tiles = ctx->tiles4k.as<int64_t>();
@@ -1004,7 +1007,7 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
                 e.t_tiles = ctx->has_test ? ctx->t_tiles4k.as<int64_t>() : nullptr;
                 e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles4k : 0;
             }
-            const bool exact = var == 0 || var == 1 || var == 3 || var == 8 || var == 12 || var == 13;  // the rest are timing diagnostics
+            const bool exact = var == 0 || var == 1 || var == 3 || var == 8 || (var >= 12 && var <= 18);  // the rest are timing diagnostics
             e.row_xw = exact ? ctx->row_xw.as<double>() : nullptr;
             launch_eval4(var, e, eval4_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
             ctx->xw_cached = exact;  // the next round's plan reuses these x.w (stream order)

@@ -346,7 +346,21 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 // GATHER: 1 = w gathered from global (the product); diagnostics (wrong values,
 // timing only): 0 = no gather, 2 = 1 lane in 8 gathers, 3 = gathered from a
 // 2048-double LDS copy of the head of w.
-template <int TILE, int BLOCK, int GATHER>
+// SAUX >= 0: the tile stream goes through buffer loads with that cache-policy
+// word (16 = sc1: bypasses the CU's L1, so the stream does not evict the
+// gathered head of w; 2 = nt; 18 = sc1 + nt) instead of nontemporal globals.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int AUX>
+__device__ __forceinline__ u32x4 stream_ld128(const void* base, int32_t voff) {
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)p);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(p >> 32));
+    void* pu = (void*)(((uint64_t)hi << 32) | lo);
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(pu, (short)0, 0x7FFFFFF0, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, AUX);
+}
+
+template <int TILE, int BLOCK, int GATHER, int SAUX = -1>
 __global__ __launch_bounds__(BLOCK) void eval_v4_kernel(EvalArgs a) {
     constexpr int UNITS = TILE / (4 * BLOCK);  // 4-entry units per thread (base alignment adds one)
     __shared__ double prod[TILE + 4];
@@ -409,9 +423,19 @@ __global__ __launch_bounds__(BLOCK) void eval_v4_kernel(EvalArgs a) {
             v0[u] = f64x2{0.0, 0.0};
             v1[u] = v0[u];
             if (k < span) {
-                c[u] = __builtin_nontemporal_load((const i32x4*)(cl + base + k));
-                v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
-                v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
+                if (SAUX >= 0) {
+                    c[u] = __builtin_bit_cast(i32x4, stream_ld128<SAUX < 0 ? 0 : SAUX>(cl + base, (int32_t)(4 * k)));
+                    v0[u] = __builtin_bit_cast(f64x2, stream_ld128<SAUX < 0 ? 0 : SAUX>(vl + base, (int32_t)(8 * k)));
+                    v1[u] = __builtin_bit_cast(f64x2, stream_ld128<SAUX < 0 ? 0 : SAUX>(vl + base, (int32_t)(8 * k + 16)));
+                } else if (SAUX == -2) {  // plain global loads (default cache policy)
+                    c[u] = *(const i32x4*)(cl + base + k);
+                    v0[u] = *(const f64x2*)(vl + base + k);
+                    v1[u] = *(const f64x2*)(vl + base + k + 2);
+                } else {
+                    c[u] = __builtin_nontemporal_load((const i32x4*)(cl + base + k));
+                    v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
+                    v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
+                }
             }
         }
 #pragma unroll
@@ -623,6 +647,16 @@ void launch_eval4(int variant, const EvalArgs& a, int blocks, hipStream_t s) {
         eval_v4_kernel<4096, 512, 6><<<blocks, 512, 0, s>>>(a);
     else if (variant == 12)
         eval_v7_kernel<4096, 512><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 14)
+        eval_v4_kernel<4096, 512, 1, 16><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 15)
+        eval_v4_kernel<4096, 512, 1, 18><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 16)
+        eval_v4_kernel<4096, 512, 1, 2><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 17)
+        eval_v4_kernel<4096, 512, 1, 0><<<blocks, 512, 0, s>>>(a);
+    else if (variant == 18)
+        eval_v4_kernel<4096, 512, 1, -2><<<blocks, 512, 0, s>>>(a);
     else if (variant == 13)
         eval_v7_kernel<4096, 256><<<blocks, 256, 0, s>>>(a);
     else

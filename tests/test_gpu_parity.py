@@ -319,7 +319,8 @@ def _eval_edge_data(seed=11):
 
 @pytest.mark.parametrize("version,variant", [("v1", "3"), ("v4", "0"), ("v4", "1"), ("v4", "3"),
                                              ("v6", "0"), ("v6", "1"), ("v6", "2"), ("v6", "3"),
-                                             ("v4", "12"), ("v4", "13")])
+                                             ("v4", "12"), ("v4", "13"), ("v4", "14"), ("v4", "15"), ("v4", "16"),
+                                             ("v4", "17"), ("v4", "18")])
 def test_fast_eval_versions_match_oracle(version, variant, monkeypatch):
     """Every fast eval kernel (OptUtils.scala:57-98) against the oracle on the
     same (w, alpha), including rows longer than a tile and empty rows."""
