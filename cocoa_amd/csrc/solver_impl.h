@@ -36,6 +36,18 @@ __device__ __forceinline__ int find_step(int32_t p, int32_t excl, int m) {
     return lo;
 }
 
+// The loader streams every sampled row's (col, val) once per round (614 MB on
+// C2).  Nontemporal loads keep that stream from evicting the partitions'
+// private deltaW slices, which the step chain gathers from L2.
+#ifndef COCOA_LOADER_NT
+#define COCOA_LOADER_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T stream_ld(const T* p) {
+    if (COCOA_LOADER_NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
 template <int MODE, bool STRICT>
 __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& cursor, BatchMeta* mb, int32_t* scol,
                            double* sval, double* prod) {
@@ -127,8 +139,8 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
             if (p < T) {
                 const int j = own[u];
                 const int64_t e = mb->beg[j] + (p - mb->off[j]);
-                pc[u] = a.col[e];
-                pv[u] = a.val[e];
+                pc[u] = stream_ld(a.col + e);
+                pv[u] = stream_ld(a.val + e);
             }
         }
         if (MODE != MODE_COCOA && !planned) {
