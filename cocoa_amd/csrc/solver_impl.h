@@ -68,14 +68,14 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
     const bool planned = a.plan_beg != nullptr;
     if (valid) {
         const size_t g = (size_t)k * H + s;
-        idx = a.samples[g];
+        idx = stream_ld(a.samples + g);
         const int64_t gr = p0 + idx;
         if (planned) {
-            beg = a.plan_beg[g];
-            z = a.plan_z[g];
-            yv = a.plan_y[g];
-            qv = a.plan_q[g];
-            if (MODE != MODE_COCOA) pxw = a.plan_xw[g];
+            beg = stream_ld(a.plan_beg + g);
+            z = stream_ld(a.plan_z + g);
+            yv = stream_ld(a.plan_y + g);
+            qv = stream_ld(a.plan_q + g);
+            if (MODE != MODE_COCOA) pxw = stream_ld(a.plan_xw + g);
         } else {
             beg = a.row_ptr[gr];
             z = a.row_ptr[gr + 1] - beg;
