@@ -510,10 +510,16 @@ void launch_solver2_impl(int mode, const Solver2Args& a, int grid, size_t lds, h
 // label, ||x||^2 and x.w (w is read-only within a round for CoCoA+ and MbCD).
 // STRICT: one lane per step, x.w summed sequentially in stored order (the
 // reference's SparseVector.dot); fast: 16 lanes per step, DPP row sum, FMA.
+// One thread per step when no dot is formed here (strict, x.w reused from the
+// eval, or CoCoA), 16 otherwise; plan_threads_per_step is the shared rule.
+__host__ __device__ __forceinline__ int plan_threads_per_step(bool strict, const PlanArgs& a) {
+    return (strict || !a.need_xw || a.xw_cache) ? 1 : 16;
+}
+
 template <bool STRICT>
 __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     const int tid = threadIdx.x;
-    const int per = STRICT ? 1 : 16;
+    const int per = plan_threads_per_step(STRICT, a);
     const int64_t g = (int64_t)blockIdx.x * (256 / per) + tid / per;
     const int sub = tid % per;
     const bool valid = g < a.steps;
@@ -533,18 +539,18 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
             xw = row16_sum(acc);
         }
     }
-    if (valid && sub == 0) {
-        a.beg[g] = b;
-        a.z[g] = (int32_t)(e - b);
-        a.py[g] = a.y[gr];
-        a.pq[g] = a.sqn[gr];
-        a.xw[g] = xw;
+    if (valid && sub == 0) {  // read once by the solver's loader: nontemporal, like its reads
+        __builtin_nontemporal_store(b, a.beg + g);
+        __builtin_nontemporal_store((int32_t)(e - b), a.z + g);
+        __builtin_nontemporal_store(a.y[gr], a.py + g);
+        __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
+        __builtin_nontemporal_store(xw, a.xw + g);
     }
 }
 
 template <bool STRICT>
 void launch_plan_impl(const PlanArgs& a, hipStream_t s) {
-    const int per = STRICT ? 1 : 16;
+    const int per = plan_threads_per_step(STRICT, a);
     const int64_t blocks = (a.steps * per + 255) / 256;
     if (blocks > 0) plan_kernel<STRICT><<<(unsigned)blocks, 256, 0, s>>>(a);
 }
