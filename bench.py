@@ -197,11 +197,8 @@ def main():
     # tools/pmc_summary.py -> profiles/traffic.json), used only when the PMC run
     # profiled the same kernel variant this run launched
     plan = eng.plan()
-    solver_tag = "solver2_kernel" if plan.get("solver") == "v2" else "solver_kernel<"
-    v4_tag = {"18": "eval_v4_kernel<4096, 512, 1, -2>"}.get(os.environ.get("COCOA_EVAL4", "3"),
-                                                            "eval_v4_kernel<4096, 512, 1, -1>")
-    eval_tag = {"v1": "eval_fast_kernel", "v2": "eval_pf_kernel<1024", "v3": "eval_pf_kernel<256",
-                "v4": v4_tag}.get(os.environ.get("COCOA_EVAL", "v4"), v4_tag)
+    solver_tag = "solver_kernel<"
+    eval_tag = "eval_stream_kernel<"
     traffic = traffic_eval = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tf) and not args.strict:

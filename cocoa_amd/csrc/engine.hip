@@ -11,7 +11,11 @@
 // with -ffp-contract=off like the strict kernels.
 #include <hip/hip_runtime.h>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -87,7 +91,7 @@ struct cocoa_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     std::string err;
-    std::string ckpt_dir;
+    std::string ckpt_dir;  // cocoa_set_checkpoint_dir: periodic (t, w, alpha) saves in cocoa_run
     // Double-buffered deltaW slices (large K_loc * d, e.g. C4): round t works in
     // set t & 1; the set round t folded is re-zeroed by a memset on zstream
     // that starts with round t+1 (after round t's eval, so the bandwidth-bound
@@ -97,7 +101,7 @@ struct cocoa_ctx {
     hipStream_t zstream = nullptr;
     hipEvent_t zdone[2] = {nullptr, nullptr}, folded = nullptr;
     bool zpending[2] = {false, false};
-    int zero_owed = -1;  // set folded last round, re-zeroed once the next round starts  // cocoa_set_checkpoint_dir: periodic (t, w, alpha) saves in cocoa_run
+    int zero_owed = -1;  // set folded last round, re-zeroed once the next round starts
 
     // training data (this rank)
     int32_t K_loc = 0, K_glob = 0, part_begin = 0, d = 0;
@@ -109,11 +113,9 @@ struct cocoa_ctx {
     // test data (this rank)
     Csr te;
     bool has_test = false;
-    // row tiles of the fast evaluation pass
-    DevBuf tiles, t_tiles, tiles4k, t_tiles4k;  // kEvalTile and 4096-entry tiles (eval v4)
-    int64_t n_tiles = 0, n_t_tiles = 0, n_tiles4k = 0, n_t_tiles4k = 0;
-    DevBuf tilesw[3], t_tilesw[3];  // wave tiles (eval v6), caps 256 / 512 / 1024 entries
-    int64_t n_tilesw[3] = {0, 0, 0}, n_t_tilesw[3] = {0, 0, 0};
+    // row tiles of the fast evaluation pass (kEvalTile entries)
+    DevBuf tiles, t_tiles;
+    int64_t n_tiles = 0, n_t_tiles = 0;
     // device feature order (see cocoa_set_train)
     std::vector<int32_t> perm, inv;
     std::vector<int64_t> n_hot_nnz;
@@ -139,14 +141,11 @@ struct cocoa_ctx {
     double* h_eval = nullptr;  // pinned [4]
     int64_t samples_cap = 0;
 
-    // solver plan (v1: CoCoA, unit fallbacks)
+    // solver plan (LDS placement) and the per-step plan of the SDCA methods
     bool vec_lds = false, alpha_lds = false;
     size_t lds_bytes = 0;
     SolverArgs sa{};
-    // solver plan (v2: CoCoA+ / MbCD)
-    bool use_v2 = false, use_plan = false;
-    size_t lds2_bytes = 0;
-    Solver2Args sa2{};
+    bool use_plan = false;
     DevBuf plan_beg, plan_z, plan_y, plan_q, plan_xw;
     // x.w of every train row for the current w, written by the fast eval pass
     // (eval v4) and reused by the next round's plan; false once w moves
@@ -437,8 +436,6 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s);
-    ctx->n_tiles4k = make_tiles(row_ptr, n_rows, ctx->tiles4k, s, 4096);
-    for (int i = 0; i < 3; ++i) ctx->n_tilesw[i] = make_tiles(row_ptr, n_rows, ctx->tilesw[i], s, 256 << i);
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
     CAPI_END(ctx)
@@ -461,8 +458,6 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s);
-    ctx->n_t_tiles4k = make_tiles(row_ptr, n_rows, ctx->t_tiles4k, s, 4096);
-    for (int i = 0; i < 3; ++i) ctx->n_t_tilesw[i] = make_tiles(row_ptr, n_rows, ctx->t_tilesw[i], s, 256 << i);
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     if (ctx->inited) {
@@ -519,130 +514,15 @@ static void plan_solver(cocoa_ctx* c) {
     a.stream_cap = (int32_t)cap;
 }
 
-static size_t pow2_at_least(size_t x) {
-    size_t p = 32;
-    while (p < x) p <<= 1;
-    return p;
-}
-
-// LDS carve of the v2 solver: hot deltaW slice + double-buffered (col, val,
-// cold) streams + batch metadata + dirty bitmaps.  All of d goes to LDS when
-// it fits (then no cold stream); otherwise the hot slice takes what is left
-// after a 1024-entry stream.
-static void plan_solver2(cocoa_ctx* c, int32_t max_nl) {
-    Solver2Args& a = c->sa2;
-    const size_t budget = kLdsMax;
-    const size_t meta = 2 * align16(sizeof(Batch2));
-    const size_t scratch = align16(sizeof(double) * kRegChunks * 64) + 64 * sizeof(double);  // + sink
-    const size_t nb_a = std::min<size_t>(pow2_at_least((size_t)std::max(max_nl, 1)), 65536);
-    const size_t abytes = 2 * align16(nb_a / 8);
-    const size_t d = (size_t)c->d;
-    size_t hot, cap, nb_w;
-    bool cold;
-    const size_t fixed_nocold = meta + scratch + abytes + 2 * align16(4);
-    if (align16(d * 8) + fixed_nocold + 2 * 1024 * 12 <= budget) {
-        cold = false;
-        hot = d;
-        nb_w = 32;
-        cap = (budget - align16(d * 8) - fixed_nocold) / 24;   // 2 buffers x (4 + 8) B
-        cap = std::min<size_t>(cap & ~(size_t)63, 8192);
-        cap = std::max<size_t>(cap, (size_t)std::min<int32_t>(c->max_z, 8192) & ~(size_t)63);
-        while (align16(d * 8) + fixed_nocold + 2 * (align16(cap * 4) + align16(cap * 8)) > budget) cap -= 64;
-    } else {
-        cold = true;
-        cap = 1024;
-        const size_t fixed = meta + scratch + abytes + 2 * (align16(cap * 4) + 2 * align16(cap * 8));
-        nb_w = std::min<size_t>(pow2_at_least(d), 65536);
-        for (int it = 0; it < 3; ++it) {
-            hot = (budget - fixed - 2 * align16(nb_w / 8)) / 8;
-            hot &= ~(size_t)15;
-            hot = std::min(hot, d);
-            nb_w = std::min<size_t>(pow2_at_least(d - hot), 65536);
-        }
-        hot = (budget - fixed - 2 * align16(nb_w / 8)) / 8;
-        hot = std::min(hot & ~(size_t)15, d);
-    }
-    size_t off = 0;
-    a.lds_hot = (int32_t)off;
-    off += align16(hot * 8);
-    for (int b = 0; b < 2; ++b) {
-        a.lds_dirty_w[b] = (int32_t)off;
-        off += align16(nb_w / 8);
-        a.lds_dirty_a[b] = (int32_t)off;
-        off += align16(nb_a / 8);
-        a.lds_col[b] = (int32_t)off;
-        off += align16(cap * 4);
-        a.lds_val[b] = (int32_t)off;
-        off += align16(cap * 8);
-        if (cold) {
-            a.lds_cold[b] = (int32_t)off;
-            off += align16(cap * 8);
-        } else {
-            a.lds_cold[b] = -1;
-        }
-        a.lds_batch[b] = (int32_t)off;
-        off += align16(sizeof(Batch2));
-    }
-    a.lds_scratch = (int32_t)off;
-    a.lds_sink = (int32_t)(off + align16(sizeof(double) * kRegChunks * 64));
-    off += scratch;
-    if (off > budget) throw Error(COCOA_E_ARG, "v2 solver LDS plan exceeds 160 KiB");
-    a.hot = (int32_t)hot;
-    a.cap = (int32_t)cap;
-    a.wmask = (int32_t)(nb_w - 1);
-    a.amask = (int32_t)(nb_a - 1);
-    c->lds2_bytes = off;
-}
-
-// fast eval kernel: COCOA_EVAL=v4 (default: 16-byte tile stream, variant
-// COCOA_EVAL4, default 3 = 4096-entry tiles, 512 threads, 3 blocks per CU),
-// v1 (4/8-byte tile stream), v2 (hot w in LDS + tile prefetch, one block per
-// CU), v3 (tile prefetch, 6 blocks per CU).  Measured on C2 (r01): v4 0.212 ms,
-// v1 0.236 ms, v2 0.320 ms, v3 0.274 ms; v4 without the w gather (diagnostic
-// variant 2) 0.104 ms, so the gather of w costs ~45% of the pass.
-static int eval_version() {
-    const char* e = std::getenv("COCOA_EVAL");
-    if (e && std::strcmp(e, "v1") == 0) return 1;
-    if (e && std::strcmp(e, "v2") == 0) return 2;
-    if (e && std::strcmp(e, "v3") == 0) return 3;
-    if (e && std::strcmp(e, "v6") == 0) return 6;
-    return 4;
-}
-
-// v2 is opt-in (COCOA_SOLVER=v2): on C2 it measured 10.5 ms/round against
-// v1's 9.8 ms (profiles/r01_bench_v2.json), so v1 stays the default.
-// fast CoCoA+/MbCD step chain: v3 (pipelined, branch-free) unless COCOA_CHAIN=v1
 // Register chunks of chain v3 (rows with z <= 64 * chunks keep their entries in
 // registers).  Measured on MI355X (r01, profiles/r01/regchunks/), C5 MbCD
 // (mean row 75.6): 6.73 ms per round with 4 chunks, 6.34 with 3, 6.09 with 2;
 // C2 CoCoA+: 3 is neutral (+0.1% in a same-box A/B), 2 is +0.7%; C4 CoCoA+
 // (mean 116): 3 is +2%.  So MbCD on short rows takes short_row_chunks (2) and
-// everything else kRegChunks.  COCOA_REG_CHUNKS_RT = short / full forces one.
+// everything else kRegChunks.
 static int reg_chunks_for(int64_t nnz, int64_t rows, int method) {
     const int mode = method == COCOA_METHOD_MBCD ? MODE_MBCD : method == COCOA_METHOD_COCOA ? MODE_COCOA : MODE_PLUS;
-    const int short_rc = short_row_chunks(mode, false);
-    const char* e = std::getenv("COCOA_REG_CHUNKS_RT");
-    if (e && std::strcmp(e, "short") == 0) return short_rc;
-    if (e && std::strcmp(e, "full") == 0) return kRegChunks;
-    return (mode == MODE_MBCD && rows > 0 && nnz <= 96 * rows) ? short_rc : kRegChunks;
-}
-
-static int chain_version() {
-    const char* e = std::getenv("COCOA_CHAIN");
-    return (e && std::strcmp(e, "v1") == 0) ? 1 : 3;
-}
-
-// per-step plan for the v1 solver's loader: on unless COCOA_PLAN=0.  r01 on
-// MI355X: C2 9.41 -> 9.35 ms per step (plan 0.34 ms, solver -0.40 ms), C3
-// 109.6 -> 86.8 ms per step.
-static bool plan_enabled() {
-    const char* e = std::getenv("COCOA_PLAN");
-    return !(e && std::strcmp(e, "0") == 0);
-}
-
-static bool v2_enabled() {
-    const char* e = std::getenv("COCOA_SOLVER");
-    return e && std::strcmp(e, "v2") == 0;
+    return (mode == MODE_MBCD && rows > 0 && nnz <= 96 * rows) ? short_row_chunks(mode, false) : kRegChunks;
 }
 
 static bool dw_double_buffer(size_t bytes);
@@ -686,7 +566,14 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     ctx->zpending[0] = ctx->zpending[1] = false;
     ctx->zero_owed = -1;
     ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * d), s);
+    // a second deltaW set only when it fits next to everything else (with 1 GiB
+    // to spare); otherwise single buffering with the zero-in-fold path
     ctx->dw_dbuf = dw_double_buffer((size_t)(K * d) * sizeof(double));
+    if (ctx->dw_dbuf) {
+        size_t free_b = 0, total_b = 0;
+        HIPCHK(hipMemGetInfo(&free_b, &total_b));
+        if (free_b < sizeof(double) * (size_t)(K * d) + ((size_t)1 << 30)) ctx->dw_dbuf = false;
+    }
     if (ctx->dw_dbuf) {
         ctx->dw2.alloc_zero(sizeof(double) * (size_t)(K * d), s);
         if (!ctx->zstream) {
@@ -730,61 +617,30 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.H = H;
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 0;
-    a.chain = chain_version();
     a.reg_chunks = reg_chunks_for(ctx->tr.nnz, ctx->tr.n, ctx->method);
     a.prof = nullptr;
     a.lam_n = params->lambda * (double)params->n;
     a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
     a.scaling = ctx->scaling;
 
-    ctx->use_v2 = v2_enabled() && (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_MBCD);
-    // v1 solver fed by the per-step plan (default; COCOA_PLAN=0 turns it off): SDCA methods only
-    ctx->use_plan = !ctx->use_v2 && plan_enabled() && is_sdca(method);
+    // the loader of the SDCA solvers is fed by the per-step plan
+    ctx->use_plan = is_sdca(method);
     a.plan_beg = nullptr;
     a.plan_z = nullptr;
     a.plan_y = a.plan_q = a.plan_xw = nullptr;
-    if (ctx->use_v2 || ctx->use_plan) {
+    if (ctx->use_plan) {
         const size_t steps = (size_t)std::max<int64_t>((int64_t)K * H, 1);
         ctx->plan_beg.alloc(steps * sizeof(int64_t));
         ctx->plan_z.alloc(steps * sizeof(int32_t));
         ctx->plan_y.alloc(steps * sizeof(double));
         ctx->plan_q.alloc(steps * sizeof(double));
         ctx->plan_xw.alloc(steps * sizeof(double));
-    }
-    if (ctx->use_plan) {
         a.plan_beg = ctx->plan_beg.as<int64_t>();
         a.plan_z = ctx->plan_z.as<int32_t>();
         a.plan_y = ctx->plan_y.as<double>();
         a.plan_q = ctx->plan_q.as<double>();
         a.plan_xw = ctx->plan_xw.as<double>();
-    }
-    if (ctx->use_v2) {
-        plan_solver2(ctx, ctx->max_nl);
-        Solver2Args& b = ctx->sa2;
-        b.row_ptr = a.row_ptr;
-        b.col = a.col;
-        b.val = a.val;
-        b.rowflags = a.rowflags;
-        b.part_ptr = a.part_ptr;
-        b.samples = a.samples;
-        b.plan_beg = ctx->plan_beg.as<int64_t>();
-        b.plan_z = ctx->plan_z.as<int32_t>();
-        b.plan_y = ctx->plan_y.as<double>();
-        b.plan_q = ctx->plan_q.as<double>();
-        b.plan_xw = ctx->plan_xw.as<double>();
-        b.alpha = a.alpha;
-        b.alpha_work = a.alpha_work;
-        b.dw = a.dw;
-        b.d = d;
-        b.H = H;
-        b.any_dup = a.any_dup;
-        b.raw_alpha = 0;
-        b.dbg_serial = std::getenv("COCOA_DBG_SERIAL") ? 1 : 0;
-        b.lam_n = a.lam_n;
-        b.sigma = a.sigma;
-        b.scaling = a.scaling;
-        b.prof = nullptr;
-    } else if (!ctx->use_plan) {
+    } else {
         ctx->plan_beg.free();
         ctx->plan_z.free();
         ctx->plan_y.free();
@@ -798,7 +654,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
 
 // Double-buffer the deltaW slices when a dense fold's zeroing pass is large:
 // K_loc * d * 8 >= 1 GiB (C4: 1,024 x 3.23 M doubles = 26.5 GB per set).
-// COCOA_DW_DBUF=0 / 1 forces it off / on.
+// COCOA_DW_DBUF=0 / 1 forces it off / on (tests); cocoa_init still falls back
+// to one set when the second does not fit in device memory.
 static bool dw_double_buffer(size_t bytes) {
     const char* e = std::getenv("COCOA_DW_DBUF");
     if (e) return std::atoi(e) != 0;
@@ -820,17 +677,13 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         c->zpending[set] = false;
     }
     c->sa.dw = dws;
-    c->sa2.dw = dws;
     if (c->zero_owed >= 0) {
         double* zs = c->zero_owed ? c->dw2.as<double>() : c->dw.as<double>();
         HIPCHK(hipEventRecord(c->folded, s));
         HIPCHK(hipStreamWaitEvent(c->zstream, c->folded, 0));
-        const char* zb = std::getenv("COCOA_ZERO_WGS");
-        const int blocks = zb ? std::atoi(zb) : 0;  // 0: hipMemsetAsync (C4: 22.8-23.3 ms/round; 64-128 WGs of zero_kernel: 23.0)
-        if (blocks > 0)
-            launch_zero(zs, (int64_t)K * d, blocks, c->zstream);
-        else
-            HIPCHK(hipMemsetAsync(zs, 0, sizeof(double) * (size_t)K * (size_t)d, c->zstream));
+        // hipMemsetAsync: C4 22.8-23.3 ms/round; a narrow zero_kernel grid (64-128
+        // workgroups) measured 23.0 (r01), so the plain memset stays
+        HIPCHK(hipMemsetAsync(zs, 0, sizeof(double) * (size_t)K * (size_t)d, c->zstream));
         HIPCHK(hipEventRecord(c->zdone[c->zero_owed], c->zstream));
         c->zpending[c->zero_owed] = true;
         c->zero_owed = -1;
@@ -839,7 +692,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         c->timed(COCOA_K_SAMPLE, [&] {
             launch_sampler(c->part_ptr.as<int64_t>(), K, seed, H, c->samples.as<int32_t>(), c->jump.as<uint64_t>(), s);
         });
-        if (c->use_v2 || c->use_plan) {
+        if (c->use_plan) {
             PlanArgs pa{};
             pa.part_ptr = c->part_ptr.as<int64_t>();
             pa.samples = c->samples.as<int32_t>();
@@ -865,14 +718,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
                     launch_plan_fast(pa, s);
             });
         }
-        if (c->use_v2) {
-            c->timed(COCOA_K_SOLVER, [&] {
-                if (c->strict)
-                    launch_solver2_strict(solver_mode(c->method), c->sa2, K, c->lds2_bytes, s);
-                else
-                    launch_solver2_fast(solver_mode(c->method), c->sa2, K, c->lds2_bytes, s);
-            });
-        } else if (is_sdca(c->method)) {
+        if (is_sdca(c->method)) {
             c->timed(COCOA_K_SOLVER, [&] {
                 if (c->strict)
                     launch_solver_strict(solver_mode(c->method), c->vec_lds, c->alpha_lds, c->sa, K, c->lds_bytes, s);
@@ -993,37 +839,11 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     ctx->timed(COCOA_K_EVAL, [&] {
         if (ctx->strict)
             launch_eval_strict(e, ctx->stream);
-        else if (eval_version() == 1)
-            launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
-        else if (eval_version() == 4) {
-            const char* ev = std::getenv("COCOA_EVAL4");
-            // 3 (nontemporal stream) stays the default: plain loads (18) make the pass
-            // 7% faster (0.210 vs 0.227 ms on C2) but leave the CSR in L2/MALL, and
-            // the next round's solver then runs 0.06 ms slower (profiles/r01/evalab/)
-            const int var = ev ? std::atoi(ev) : 3;
-            if (eval4_tile(var) == 4096) {  // v4 variant tiles
-                e.tiles = ctx->tiles4k.as<int64_t>();
-                e.n_tiles = ctx->n_tiles4k;
-                e.t_tiles = ctx->has_test ? ctx->t_tiles4k.as<int64_t>() : nullptr;
-                e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles4k : 0;
-            }
-            const bool exact = var == 0 || var == 1 || var == 3 || var == 8 || (var >= 12 && var <= 18);  // the rest are timing diagnostics
-            e.row_xw = exact ? ctx->row_xw.as<double>() : nullptr;
-            launch_eval4(var, e, eval4_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
-            ctx->xw_cached = exact;  // the next round's plan reuses these x.w (stream order)
-        } else if (eval_version() == 6) {
-            const char* ev = std::getenv("COCOA_EVAL6");
-            const int var = ev ? std::atoi(ev) : 0;
-            const int ti = eval6_tile(var) == 256 ? 0 : eval6_tile(var) == 512 ? 1 : 2;
-            e.tiles = ctx->tilesw[ti].as<int64_t>();
-            e.n_tiles = ctx->n_tilesw[ti];
-            e.t_tiles = ctx->has_test ? ctx->t_tilesw[ti].as<int64_t>() : nullptr;
-            e.n_t_tiles = ctx->has_test ? ctx->n_t_tilesw[ti] : 0;
+        else {
             e.row_xw = ctx->row_xw.as<double>();
-            launch_eval6(var, e, eval6_blocks(var, e.n_tiles, e.n_t_tiles), ctx->stream);
-            ctx->xw_cached = true;
-        } else
-            launch_eval2(eval_version(), e, eval2_blocks(eval_version(), e.n_tiles, e.n_t_tiles), ctx->stream);
+            launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
+            ctx->xw_cached = true;  // the next round's plan reuses these x.w (stream order)
+        }
     });
     HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1071,9 +891,30 @@ extern "C" int cocoa_run(cocoa_ctx* ctx, const cocoa_params* params, const cocoa
     return run_rounds(ctx, params, 0, cb, user);
 }
 
+// mkdir -p: sc.setCheckpointDir (hingeDriver.scala:56) creates the directory,
+// so a missing one is created here, and an unusable one fails now rather than
+// after chkptIter rounds of work.
+static void make_dirs(const std::string& dir) {
+    std::string cur;
+    size_t i = 0;
+    while (i <= dir.size()) {
+        const size_t j = dir.find('/', i);
+        const size_t e = j == std::string::npos ? dir.size() : j;
+        cur = dir.substr(0, e);
+        if (!cur.empty() && ::mkdir(cur.c_str(), 0777) != 0 && errno != EEXIST)
+            throw Error(COCOA_E_IO, "cannot create checkpoint directory " + cur + ": " + std::strerror(errno));
+        i = e + 1;
+    }
+    struct stat st {};
+    require(::stat(dir.c_str(), &st) == 0 && S_ISDIR(st.st_mode) && ::access(dir.c_str(), W_OK) == 0, COCOA_E_IO,
+            "checkpoint directory " + dir + " is not a writable directory");
+}
+
 extern "C" int cocoa_set_checkpoint_dir(cocoa_ctx* ctx, const char* dir) {
     CAPI_BEGIN(ctx)
-    ctx->ckpt_dir = dir ? dir : "";
+    const std::string d = dir ? dir : "";
+    if (!d.empty()) make_dirs(d);
+    ctx->ckpt_dir = d;
     CAPI_END(ctx)
 }
 
@@ -1159,7 +1000,8 @@ struct CkptHeader {
     int64_t n, rows;
     double lambda, beta, gamma;
     int32_t t, pad;
-    int64_t reserved[2];
+    int32_t seed, strict;  // DebugParams.seed and the numerics mode: a resume must continue the same trajectory
+    int64_t reserved;
 };
 static_assert(sizeof(CkptHeader) == 96, "checkpoint header layout");
 
@@ -1184,6 +1026,8 @@ CkptHeader ckpt_header(const cocoa_ctx* c, int32_t t) {
     h.beta = c->P.beta;
     h.gamma = c->P.gamma;
     h.t = t;
+    h.seed = c->D.seed;
+    h.strict = c->strict ? 1 : 0;
     return h;
 }
 }  // namespace
@@ -1232,7 +1076,8 @@ extern "C" int cocoa_checkpoint_load(cocoa_ctx* ctx, const char* path, int32_t* 
     const bool same = ok && h.method == want.method && h.num_features == want.num_features &&
                       h.k_glob == want.k_glob && h.part_begin == want.part_begin && h.k_loc == want.k_loc &&
                       h.local_iters == want.local_iters && h.n == want.n && h.rows == want.rows &&
-                      h.lambda == want.lambda && h.beta == want.beta && h.gamma == want.gamma && h.t >= 0;
+                      h.lambda == want.lambda && h.beta == want.beta && h.gamma == want.gamma && h.t >= 0 &&
+                      h.seed == want.seed && h.strict == want.strict;
     if (same) {
         ok = std::fread(w.data(), sizeof(double), w.size(), f) == w.size();
         ok = ok && (ctx->tr.n == 0 || std::fread(al.data(), sizeof(double), (size_t)ctx->tr.n, f) == (size_t)ctx->tr.n);
@@ -1241,7 +1086,8 @@ extern "C" int cocoa_checkpoint_load(cocoa_ctx* ctx, const char* path, int32_t* 
     std::fclose(f);
     require(ok, COCOA_E_IO, std::string("not a COCOACK1 checkpoint or truncated: ") + path);
     require(same, COCOA_E_ARG,
-            std::string("checkpoint ") + path + " was written for a different problem, method or partitioning");
+            std::string("checkpoint ") + path +
+                " was written for a different problem, method, partitioning, seed or numerics mode");
     uint64_t sum = 1469598103934665603ULL;
     sum = fnv1a(sum, &h, sizeof h);
     sum = fnv1a(sum, w.data(), sizeof(double) * w.size());
@@ -1315,7 +1161,6 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     a.H = local_iters;
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 1;
-    a.chain = chain_version();
     a.reg_chunks = reg_chunks_for(ctx->tr.nnz, ctx->tr.n, ctx->method);
     a.prof = nullptr;
     a.lam_n = lambda * (double)n;
@@ -1390,10 +1235,8 @@ extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
     if (enable) {
         ctx->prof.alloc_zero(sizeof(uint64_t) * (size_t)ctx->K_loc * 32, ctx->stream);
         ctx->sa.prof = ctx->prof.as<uint64_t>();
-        ctx->sa2.prof = ctx->prof.as<uint64_t>();
     } else {
         ctx->sa.prof = nullptr;
-        ctx->sa2.prof = nullptr;
     }
     CAPI_END(ctx)
 }
@@ -1412,14 +1255,11 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
     require(buf && len > 0, COCOA_E_ARG, "bad buffer");
     std::snprintf(buf, (size_t)len,
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
-                  "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,\"solver\":\"%s\","
-                  "\"hot\":%d,\"cap2\":%d,\"lds2_bytes\":%zu,\"hot_nnz_frac\":%.4f}",
+                  "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
+                  "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d}",
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
-                  ctx->use_v2 ? "v2" : "v1", ctx->use_v2 ? ctx->sa2.hot : 0, ctx->use_v2 ? ctx->sa2.cap : 0,
-                  ctx->lds2_bytes,
-                  ctx->use_v2 && ctx->tr.nnz > 0
-                      ? (double)ctx->n_hot_nnz[(size_t)ctx->sa2.hot] / (double)ctx->tr.nnz
-                      : 0.0);
+                  ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,
+                  ctx->dw_dbuf ? 1 : 0);
     CAPI_END(ctx)
 }

@@ -23,7 +23,7 @@ constexpr int kRegChunks = COCOA_REG_CHUNKS;  // rows with z <= 64 * kRegChunks 
 constexpr int short_row_chunks(int mode, bool strict) {
     return (strict || mode == 1) ? kRegChunks : (mode == 2 ? (kRegChunks < 2 ? kRegChunks : 2) : (kRegChunks < 3 ? kRegChunks : 3));
 }
-constexpr int kEvalTile = 2048;     // entries (and max rows) per fast-eval tile
+constexpr int kEvalTile = 4096;     // entries (and max rows) per fast-eval tile
 
 // Per-batch step metadata, staged by the loader wave in LDS (SoA).
 struct BatchMeta {
@@ -67,7 +67,6 @@ struct SolverArgs {
     int32_t stream_cap;       // staged entries per batch buffer
     int32_t any_dup;
     int32_t raw_alpha;        // 1: write the raw local alpha (unit localSDCA API)
-    int32_t chain;            // fast CoCoA+/MbCD: 3 = pipelined branch-free step chain, 1 = v1 chain
     int32_t reg_chunks;       // chain v3: register chunks per row, kRegChunks or short_row_chunks() (engine: reg_chunks_for)
     double lam_n;             // lambda * n
     double sigma;             // sigma' = K * gamma (CoCoA+)
@@ -81,61 +80,6 @@ struct SolverArgs {
     int32_t lds_vec;          // d doubles (deltaW, or w_loc for CoCoA) if VEC_LDS
     int32_t lds_alpha;        // rows-of-largest-partition doubles if ALPHA_LDS
     uint64_t* prof;           // optional cycle counters [K][2 waves][16] (diagnostics)
-};
-
-// ---- local solver v2 (CoCoA+ / MbCD): hot deltaW slice in LDS, cold entries
-// prefetched by the loader waves, dirty bitmaps for the prefetch window.
-struct StepMeta {             // 64 B, one per step of a staged batch
-    int32_t r, off, z, fl;    // sampled row (partition-local), stream offset (-1: unstaged), nnz, flags
-    int64_t beg;              // global entry offset of the row
-    double y, q, xw, ap;      // label, Math.pow(norm(x),2), x.w (step plan), prefetched alpha_work[r]
-    int64_t pad;
-};
-struct Batch2 {
-    StepMeta st[kMetaSteps];
-    int32_t m;                // steps in this batch (0 = no more work)
-    int32_t pad[3];
-};
-
-struct Solver2Args {
-    const int64_t* row_ptr;
-    const int32_t* col;
-    const double* val;
-    const uint8_t* rowflags;
-    const int64_t* part_ptr;
-    const int32_t* samples;   // K_loc * H
-    // step plan (K_loc * H each), written by the plan kernel for this round
-    const int64_t* plan_beg;
-    const int32_t* plan_z;
-    const double* plan_y;
-    const double* plan_q;
-    const double* plan_xw;
-    double* alpha;            // alphaOld (persistent)
-    double* alpha_work;       // working alpha (rank-local rows)
-    double* dw;               // K_loc * d private deltaW (zero on entry)
-    int64_t d;
-    int32_t H;
-    int32_t hot;              // features [0, hot) of deltaW live in LDS
-    int32_t cap;              // staged entries per batch buffer
-    int32_t any_dup;
-    int32_t raw_alpha;        // 1: write the raw local alpha (unit localSDCA API)
-    int32_t wmask;            // cold-feature dirty bitmap: bit ((c - hot) & wmask)
-    int32_t amask;            // row dirty bitmap: bit (r & amask)
-    int32_t dbg_serial;       // diagnostics: loader and solver take turns (no overlap)
-    double lam_n;
-    double sigma;
-    double scaling;
-    // LDS carve (byte offsets)
-    int32_t lds_hot;
-    int32_t lds_dirty_w[2];
-    int32_t lds_dirty_a[2];
-    int32_t lds_col[2];
-    int32_t lds_val[2];
-    int32_t lds_cold[2];      // -1: no cold entries (hot == d)
-    int32_t lds_batch[2];
-    int32_t lds_scratch;
-    int32_t lds_sink;         // 64 doubles
-    uint64_t* prof;
 };
 
 struct PlanArgs {
@@ -197,20 +141,9 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
                         hipStream_t s);
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
 int eval_fast_blocks(int64_t n, int64_t n_test);
-void launch_eval2(int version, const EvalArgs& a, int blocks, hipStream_t s);
-int eval2_blocks(int version, int64_t n, int64_t n_test);
-void launch_eval4(int variant, const EvalArgs& a, int blocks, hipStream_t s);
-int eval4_blocks(int variant, int64_t n, int64_t n_test);
-int eval4_tile(int variant);
-void launch_eval6(int variant, const EvalArgs& a, int blocks, hipStream_t s);
-int eval6_blocks(int variant, int64_t n, int64_t n_test);
-int eval6_tile(int variant);
-
-void launch_solver2_fast(int mode, const Solver2Args& a, int grid, size_t lds, hipStream_t s);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 
 // strict translation unit
-void launch_solver2_strict(int mode, const Solver2Args& a, int grid, size_t lds, hipStream_t s);
 void launch_plan_strict(const PlanArgs& a, hipStream_t s);
 void launch_solver_strict(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
                           hipStream_t s);

@@ -4,7 +4,7 @@
 // the shared state (sampler, deltaW fold, w apply, strict evaluation, SGD).
 #include "jrandom.h"
 #include "kernels.h"
-#include "solver2_impl.h"
+#include "plan_impl.h"
 #include "solver_impl.h"
 #include "wave.h"
 
@@ -13,10 +13,6 @@ namespace cocoa {
 void launch_solver_strict(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
                           hipStream_t s) {
     launch_solver_impl<true>(mode, vec_lds, alpha_lds, a, grid, lds, s);
-}
-
-void launch_solver2_strict(int mode, const Solver2Args& a, int grid, size_t lds, hipStream_t s) {
-    launch_solver2_impl<true>(mode, a, grid, lds, s);
 }
 
 void launch_plan_strict(const PlanArgs& a, hipStream_t s) { launch_plan_impl<true>(a, s); }

@@ -1,0 +1,61 @@
+// Per-round step plan, shared by the strict and fast translation units.
+//
+// For every step (k, s) of the round: the sampled row's entry offset, nnz,
+// label, ||x||^2 and x.w (w is read-only within a round for CoCoA+ and MbCD,
+// CoCoA.scala:159 / MinibatchCD.scala:104).  One chip-wide pass, so the local
+// solvers' loader waves read one coalesced record per step instead of the
+// samples -> row_ptr -> (col, val) -> w chain.
+// STRICT: one lane per step, x.w summed sequentially in stored order (the
+// reference's SparseVector.dot); fast: 16 lanes per step, DPP row sum, FMA.
+// One thread per step when no dot is formed here (strict, x.w reused from the
+// eval, or CoCoA), 16 otherwise; plan_threads_per_step is the shared rule.
+#pragma once
+#include "kernels.h"
+#include "wave.h"
+
+namespace cocoa {
+
+__host__ __device__ __forceinline__ int plan_threads_per_step(bool strict, const PlanArgs& a) {
+    return (strict || !a.need_xw || a.xw_cache) ? 1 : 16;
+}
+
+template <bool STRICT>
+__global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
+    const int tid = threadIdx.x;
+    const int per = plan_threads_per_step(STRICT, a);
+    const int64_t g = (int64_t)blockIdx.x * (256 / per) + tid / per;
+    const int sub = tid % per;
+    const bool valid = g < a.steps;
+    const int64_t gg = valid ? g : 0;
+    const int32_t k = (int32_t)(gg / a.H);
+    const int64_t gr = a.part_ptr[k] + a.samples[gg];
+    const int64_t b = a.row_ptr[gr], e = a.row_ptr[gr + 1];
+    double xw = 0.0;
+    if (a.need_xw && a.xw_cache) {
+        xw = valid ? a.xw_cache[gr] : 0.0;  // the last eval pass already formed x.w for this w
+    } else if (a.need_xw) {
+        if (STRICT) {
+            for (int64_t q = b; q < e; ++q) xw += a.val[q] * a.w[a.col[q]];
+        } else {
+            double acc = 0.0;
+            for (int64_t q = b + sub; q < e; q += 16) acc += a.val[q] * a.w[a.col[q]];
+            xw = row16_sum(acc);
+        }
+    }
+    if (valid && sub == 0) {  // read once by the solver's loader: nontemporal, like its reads
+        __builtin_nontemporal_store(b, a.beg + g);
+        __builtin_nontemporal_store((int32_t)(e - b), a.z + g);
+        __builtin_nontemporal_store(a.y[gr], a.py + g);
+        __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
+        __builtin_nontemporal_store(xw, a.xw + g);
+    }
+}
+
+template <bool STRICT>
+void launch_plan_impl(const PlanArgs& a, hipStream_t s) {
+    const int per = plan_threads_per_step(STRICT, a);
+    const int64_t blocks = (a.steps * per + 255) / 256;
+    if (blocks > 0) plan_kernel<STRICT><<<(unsigned)blocks, 256, 0, s>>>(a);
+}
+
+}  // namespace cocoa

@@ -612,7 +612,7 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
             load_batch<MODE, STRICT>(a, k, p0, cursor, (BatchMeta*)(lds + a.lds_meta[cur ^ 1]),
                                      (int32_t*)(lds + a.lds_stream_col[cur ^ 1]), (double*)(lds + a.lds_stream_val[cur ^ 1]),
                                      prod);
-        } else if (!STRICT && MODE != MODE_COCOA && a.chain == 3) {
+        } else if (!STRICT && MODE != MODE_COCOA) {
             compute_batch3<MODE, VEC_LDS, RC>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
                                               (const double*)(lds + a.lds_stream_val[cur]), vec, alv);
         } else {

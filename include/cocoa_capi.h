@@ -151,11 +151,12 @@ int cocoa_set_alpha(cocoa_ctx *ctx, const double *alpha_in);
  * (CoCoA.scala:58-62); here the round state goes to a file so that a long run
  * (config C4) can stop and resume.  Format "COCOACK1", little-endian: a
  * 96-byte header (method, n, num_features, K_glob, part_begin, K_loc, rows,
- * local_iters, lambda, beta, gamma, t), w[num_features] in original feature
- * order, alpha[rows], then an FNV-1a 64 checksum of everything before it.
- * Load validates the header against the context (same problem, method and
- * partitioning; COCOA_E_ARG otherwise) and the checksum (COCOA_E_IO), sets w
- * and alpha, and returns the round t to resume after. */
+ * local_iters, lambda, beta, gamma, t, seed, strict), w[num_features] in
+ * original feature order, alpha[rows], then an FNV-1a 64 checksum of
+ * everything before it.  Load validates the header against the context (same
+ * problem, method, partitioning, DebugParams.seed and numerics mode;
+ * COCOA_E_ARG otherwise) and the checksum (COCOA_E_IO), sets w and alpha, and
+ * returns the round t to resume after. */
 int cocoa_checkpoint_save(cocoa_ctx *ctx, const char *path, int32_t t);
 int cocoa_checkpoint_load(cocoa_ctx *ctx, const char *path, int32_t *t_out);
 /* Periodic checkpoints inside cocoa_run / cocoa_resume: with a directory set
@@ -189,7 +190,7 @@ int cocoa_samples(cocoa_ctx *ctx, int32_t part, int32_t seed_plus_t, int32_t cou
 #define COCOA_K_FOLD 2
 #define COCOA_K_APPLY 3
 #define COCOA_K_EVAL 4
-#define COCOA_K_PLAN 5   /* per-round step plan (row offsets, x.w) of the v2 solver */
+#define COCOA_K_PLAN 5   /* per-round step plan (row offsets, x.w) of the SDCA loaders */
 #define COCOA_K_COUNT 6
 /* enable = 1: bracket every launch with HIP events on the context stream. */
 int cocoa_stats_enable(cocoa_ctx *ctx, int enable);

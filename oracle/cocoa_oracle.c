@@ -399,17 +399,17 @@ static void mbcd_local(const int64_t *row_ptr, const int32_t *col, const double 
         const int32_t *c = col + b;
         const double *v = val + b;
         const double yy = y[idx];
-        double grad = (yy * (sp_dot(c, v, z, w)) - 1.0) * lam_n;      /* :219 */
+        double grad = (yy * (sp_dot(c, v, z, w)) - 1.0) * lam_n;      /* MinibatchCD.scala:104 */
         double proj = grad;
         if (alpha[idx] <= 0.0) proj = jmin(grad, 0.0);
         else if (alpha[idx] >= 1.0) proj = jmax(grad, 0.0);
         if (fabs(proj) != 0.0) {
             double nr = sp_norm2(v, z);
-            double qii = nr * nr;                                     /* :229 */
+            double qii = nr * nr;                                     /* MinibatchCD.scala:114 */
             double na = 1.0;
             if (qii != 0.0) na = jmin(jmax((alpha[idx] - (grad / qii)), 0.0), 1.0);
             double coef = (yy * (na - alpha[idx])) / lam_n;
-            for (int64_t i = 0; i < z; ++i) delta_w[c[i]] += v[i] * coef; /* :236-237 */
+            for (int64_t i = 0; i < z; ++i) delta_w[c[i]] += v[i] * coef; /* MinibatchCD.scala:121-122 */
             alpha[idx] = na;
         }
     }
@@ -422,28 +422,28 @@ static void sgd_local(const int64_t *row_ptr, const int32_t *col, const double *
                       int32_t seed, double *w_scratch, double *delta_w) {
     jrand_t r;
     jr_init(&r, (int64_t)seed);
-    memcpy(w_scratch, w_init, sizeof(double) * (size_t)d);           /* :349 */
-    memset(delta_w, 0, sizeof(double) * (size_t)d);                   /* :350 */
+    memcpy(w_scratch, w_init, sizeof(double) * (size_t)d);           /* SGD.scala:100 */
+    memset(delta_w, 0, sizeof(double) * (size_t)d);                   /* SGD.scala:101 */
     for (int32_t i = 1; i <= local_iters; ++i) {
-        double step = 1.0 / (lambda * (t0 + (double)i));              /* :355 */
-        int32_t idx = jr_next_int_bound(&r, n_local);                 /* :358 */
+        double step = 1.0 / (lambda * (t0 + (double)i));              /* SGD.scala:106 */
+        int32_t idx = jr_next_int_bound(&r, n_local);                 /* SGD.scala:109 */
         const int64_t b = row_ptr[idx], z = row_ptr[idx + 1] - b;
         const int32_t *c = col + b;
         const double *v = val + b;
         const double yy = y[idx];
-        double ev = 1.0 - (yy * (sp_dot(c, v, z, w_scratch)));        /* :364 */
-        if (local) {                                                  /* :366-370 */
+        double ev = 1.0 - (yy * (sp_dot(c, v, z, w_scratch)));        /* SGD.scala:115 */
+        if (local) {                                                  /* SGD.scala:117-121 */
             double scale = 1.0 - (step * lambda);
             for (int32_t j = 0; j < d; ++j) w_scratch[j] *= scale;
         }
-        if (ev > 0) {                                                 /* :373-379 */
+        if (ev > 0) {                                                 /* SGD.scala:124-130 */
             for (int64_t q = 0; q < z; ++q) {
                 double u = v[q] * yy;
                 delta_w[c[q]] += u;
                 if (local) w_scratch[c[q]] += (u * step);
             }
         }
-        if (local)                                                    /* :381-383 */
+        if (local)                                                    /* SGD.scala:132-134 */
             for (int32_t j = 0; j < d; ++j) delta_w[j] = w_scratch[j] - w_init[j];
     }
 }
@@ -635,11 +635,11 @@ void oracle_run_local(oracle_run *R, int32_t t, double *dw_sum) {
     if (R->method == M_MBSGD || R->method == M_LOCALSGD) {
         double step = 1 / (R->lambda * (double)t);                    /* SGD.scala:44 */
         R->sgd_step = step;
-        if (R->method == M_MBSGD) {                                   /* :295-299 */
+        if (R->method == M_MBSGD) {                                   /* SGD.scala:46-50 */
             double scale = 1.0 - (step * R->lambda);
             for (int64_t j = 0; j < d; ++j) R->w[j] *= scale;
         }
-        /* ((t-1) * localIters * parts) in Scala Int arithmetic (:302) */
+        /* ((t-1) * localIters * parts) in Scala Int arithmetic (SGD.scala:53) */
         int32_t ti = (int32_t)((uint32_t)(t - 1) * (uint32_t)R->H * (uint32_t)R->Kg);
         t0 = (double)ti;
     }

@@ -317,16 +317,9 @@ def _eval_edge_data(seed=11):
                        np.concatenate([v for _, v in rows]), y, part, d)
 
 
-@pytest.mark.parametrize("version,variant", [("v1", "3"), ("v4", "0"), ("v4", "1"), ("v4", "3"),
-                                             ("v6", "0"), ("v6", "1"), ("v6", "2"), ("v6", "3"),
-                                             ("v4", "12"), ("v4", "13"), ("v4", "14"), ("v4", "15"), ("v4", "16"),
-                                             ("v4", "17"), ("v4", "18")])
-def test_fast_eval_versions_match_oracle(version, variant, monkeypatch):
-    """Every fast eval kernel (OptUtils.scala:57-98) against the oracle on the
-    same (w, alpha), including rows longer than a tile and empty rows."""
-    monkeypatch.setenv("COCOA_EVAL", version)
-    monkeypatch.setenv("COCOA_EVAL4", variant)
-    monkeypatch.setenv("COCOA_EVAL6", variant)
+def test_fast_eval_matches_oracle_edge_rows():
+    """The fast eval stream kernel (OptUtils.scala:57-98) against the oracle on
+    the same (w, alpha), including rows longer than a tile and empty rows."""
     tr = _eval_edge_data()
     te = tr.row_range(200, 1300)
     od, ot = odata(tr), odata(te)
