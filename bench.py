@@ -8,8 +8,10 @@ steps, deltaW fold, RCCL all-reduce when N > 1, w update) followed by the
 duality-gap / test-error evaluation (so the gap trajectory is measured inside
 the timed region).  value = coordinate updates per second over all GPUs.
 
-Scaling is weak: every GPU holds its own 677,399-row shard of one seeded
-problem (64 partitions each, K = 64*N globally, H unchanged).
+Scaling (cocoa_amd.configs): weak by default -- every GPU holds its own
+677,399-row shard of one seeded problem (64 partitions each, K = 64*N
+globally, H unchanged); --scaling strong keeps one fixed problem (n, K) and
+splits its partitions over the GPUs (C3: K = 64 on 1-8 GPUs; C4: K = 1,024).
 
 Prints one JSON line (rank 0).  Launch N > 1 with
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -29,28 +31,11 @@ METRIC = "CoCoA+ SVM wall-clock to duality gap 1e-4; coord updates/s at 1/2/4/8 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak
 
 
-# BASELINE.json configs.  c2 is the headline line the
-# driver runs; c3 (epsilon-shaped dense) and c4 (url-shaped, K=1024) are extra
-# measurement lines, c5 is c2 with --method over the five methods.
-_SYN = "synthetic: seeded {} generator ({}); no dataset download"
-CONFIGS = {
-    "c2": dict(kind="rcv1", n=677399, d=47236, nnz=75.6, parts=64, lam=1e-4, n_test=50000, shape="rcv1-shaped",
-               data=_SYN.format("rcv1-shaped", "Zipf columns, unit-norm tf-idf-like rows, planted separator + 10% noise")),
-    "c3": dict(kind="epsilon", n=400000, d=2000, nnz=2000.0, parts=64, lam=1e-4, n_test=10000,
-               shape="epsilon-shaped dense",
-               data=_SYN.format("epsilon-shaped", "dense N(0,1) rows, L2-normalised, planted separator")),
-    "c4": dict(kind="url", n=2396130, d=3231961, nnz=116.0, parts=1024, lam=1e-4, n_test=20000,
-               shape="url-shaped very sparse",
-               data=_SYN.format("url-shaped", "heavy-Zipf columns, ~116 nnz/row, planted separator")),
-}
+from cocoa_amd.configs import CONFIGS  # noqa: E402  (BASELINE.json configs)
 
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
-
-
-def balanced(n, K):
-    return np.array([(n * k) // K for k in range(K + 1)], np.int64)
 
 
 def solver_bytes_per_round(tr, H, seed_t, plus=True):
@@ -74,6 +59,9 @@ def main():
                     help="BASELINE.json config (c2 = the headline line; c3/c4 are extra measurement lines)")
     ap.add_argument("--method", default="cocoa+", choices=["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"],
                     help="C5 five-method comparison: the method whose rounds are timed")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: every GPU holds its own n-row shard (K = parts*N); strong: one fixed problem "
+                         "(n rows, K = parts) whose partitions are split over the GPUs")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--strict", action="store_true", help="bit-exact mode (default: fast)")
@@ -106,26 +94,22 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    import cocoa_amd
+    import cocoa_amd  # noqa: F401
+    from cocoa_amd import configs
     from cocoa_amd.dist import DistributedCoCoA, TorchEngine
 
-    # ---- data: this rank's shard of one seeded rcv1-shaped problem ----------
+    # ---- data: this rank's share of the seeded problem (cocoa_amd.configs) ----
     t0 = time.time()
-    rows = args.n + args.n_test
-    stride = ((rows + 4095) // 4096) * 4096
-    allr = cocoa_amd.gen_synthetic(cfg["kind"], rows, args.d, args.nnz, 1, 12345, first_row=rank * stride,
-                                   threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
-    tr = allr.row_range(0, args.n)
-    tr.part_ptr = balanced(args.n, args.parts)
-    te = allr.row_range(args.n, rows)
-    del allr
-    K_glob = args.parts * world
-    n_glob = args.n * world
-    H = max(int(1.0 * n_glob / K_glob), 1)  # hingeDriver.scala:70 with localIterFrac = 1
-    log(f"rank {rank}: data n={tr.n} nnz={tr.nnz} d={args.d} K={args.parts} H={H} gen {time.time() - t0:.1f}s")
+    sh = configs.share(args.config, rank=rank, world=world, scaling=args.scaling, n=args.n, d=args.d, nnz=args.nnz,
+                       parts=args.parts, lam=args.lam, n_test=args.n_test,
+                       threads=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    tr, te = sh.train, sh.test
+    K_glob, n_glob, H = sh.k_glob, sh.n_glob, sh.H
+    log(f"rank {rank}: data n={tr.n} nnz={tr.nnz} d={args.d} K_loc={tr.num_parts} K={K_glob} H={H} "
+        f"gen {time.time() - t0:.1f}s")
 
     eng = TorchEngine(device=local_rank, strict=args.strict)
-    eng.set_train(tr, part_begin=rank * args.parts, num_parts_global=K_glob)
+    eng.set_train(tr, part_begin=sh.part_begin, num_parts_global=K_glob)
     eng.set_test(te)
     eng.init(args.method, n_glob, 1 << 30, H, args.lam)
     runner = DistributedCoCoA(eng)
@@ -231,8 +215,8 @@ def main():
         for r in range(2, R + 2):
             run.round(r)
         tcpu = time.perf_counter() - tc
-        cpu = {"value": args.parts * H * R / tcpu, "unit": "coord updates/s", "cores": cores, "kind": "port",
-               "sample": f"{R} {args.method} rounds of the same {args.config.upper()} shard (K={args.parts}, H={H}) by the strict C oracle "
+        cpu = {"value": tr.num_parts * H * R / tcpu, "unit": "coord updates/s", "cores": cores, "kind": "port",
+               "sample": f"{R} {args.method} rounds of the same {args.config.upper()} shard (K={tr.num_parts}, H={H}) by the strict C oracle "
                          f"(oracle/cocoa_oracle.c), one pthread per partition group, {tcpu:.1f}s"}
         log(f"cpu baseline {cpu}")
 
@@ -240,15 +224,15 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "coord updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
             "data": cfg["data"],
-            "config": {"workload": f"{args.config.upper()} {cfg['shape']} {args.method} (n={args.n}/GPU, d={args.d}, "
-                                   f"~{args.nnz} nnz/row, lambda={args.lam}, K={args.parts}/GPU, H=n/K={H}), "
+            "config": {"workload": f"{args.config.upper()} {cfg['shape']} {args.method} (n={tr.n}/GPU of {n_glob}, d={args.d}, "
+                                   f"~{args.nnz} nnz/row, lambda={args.lam}, K={K_glob} ({tr.num_parts}/GPU), H=n/K={H}), "
                                    f"step = round + {'gap' if sdca else 'primal'} eval",
                        "method": args.method,
                        "n_total": n_glob, "K_total": K_glob, "H": H, "nnz_per_gpu": tr.nnz, "test_rows_per_gpu": te.n,
                        "mode": "strict" if args.strict else "fast",
-                       "parallelism": f"dp{world}: {args.parts} partitions per GPU, deltaW all-reduce (RCCL)"},
+                       "parallelism": f"dp{world}: {tr.num_parts} partitions per GPU, deltaW all-reduce (RCCL)"},
             "time_to_gap_s": ttg, "rounds_to_gap": rounds_to_gap, "gap_target": args.gap_target,
             "final_gap": final_gap, "gap_trajectory_timed": gaps,
             "roofline": {"kernel": "solver (local SDCA, CoCoA.localSDCA)", "bound": "hbm", "achieved": ach,
