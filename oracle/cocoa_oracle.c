@@ -477,8 +477,9 @@ double oracle_primal(const oracle_data *D, const double *w, double lambda) {
     return avg + (0.5 * lambda * (nw * nw));                          /* :73-75 */
 }
 
-/* alpha: n entries, partition-contiguous like D's rows. */
-double oracle_dual(const oracle_data *D, const double *w, const double *alpha, double lambda) {
+/* alpha: n entries, partition-contiguous like D's rows.  Per-partition
+ * DenseVector.sum, merged in partition order (alpha.map(_.sum).reduce). */
+static double alpha_sum_parts(const oracle_data *D, const double *alpha) {
     double tot = 0.0;
     int have = 0;
     for (int32_t k = 0; k < D->K; ++k) {
@@ -488,8 +489,12 @@ double oracle_dual(const oracle_data *D, const double *w, const double *alpha, d
         tot = have ? tot + s : s;
         have = 1;
     }
+    return tot;
+}
+
+double oracle_dual(const oracle_data *D, const double *w, const double *alpha, double lambda) {
     double nw = dense_norm2(w, D->d);
-    return (-lambda / 2 * (nw * nw)) + (tot / (double)D->n);          /* :80-84 */
+    return (-lambda / 2 * (nw * nw)) + (alpha_sum_parts(D, alpha) / (double)D->n); /* :80-84 */
 }
 
 double oracle_gap(const oracle_data *D, const double *w, const double *alpha, double lambda) {
@@ -689,15 +694,20 @@ void oracle_run_round(oracle_run *R, int32_t t) {
 }
 
 /* out: [primal, dual, gap, test_err_count, train_hinge_sum, alpha_sum] */
+/* P, D, gap with n = Params.n (data.count() of the whole RDD, OptUtils.scala:
+ * 65-84): equal to D->n for a full problem; for one rank's share of a larger
+ * problem the objectives are that share's terms over the global n. */
 void oracle_run_eval(const oracle_run *R, const oracle_data *test, double *out) {
-    out[0] = oracle_primal(&R->D, R->w, R->lambda);
-    out[1] = oracle_dual(&R->D, R->w, R->alpha, R->lambda);
-    out[2] = oracle_gap(&R->D, R->w, R->alpha, R->lambda);
+    const double n = (double)R->n;
+    const double h = hinge_sum(&R->D, R->w);
+    const double a = alpha_sum_parts(&R->D, R->alpha);
+    const double nw = dense_norm2(R->w, R->D.d);
+    out[0] = h / n + (0.5 * R->lambda * (nw * nw));                  /* :73-75 */
+    out[1] = (-R->lambda / 2 * (nw * nw)) + (a / n);                  /* :80-84 */
+    out[2] = out[0] - out[1];                                         /* :89-91 */
     out[3] = test ? (double)oracle_error_count(test, R->w) : -1.0;
-    out[4] = hinge_sum(&R->D, R->w);
-    double s = 0.0;
-    for (int64_t r = 0; r < R->D.n; ++r) s += R->alpha[r];
-    out[5] = s;
+    out[4] = h;
+    out[5] = a;
 }
 
 void oracle_run_get_w(const oracle_run *R, double *out) { memcpy(out, R->w, sizeof(double) * (size_t)R->D.d); }
