@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: every GPU holds its own n-row shard (K = parts*N); strong: one fixed problem "
                          "(n rows, K = parts) whose partitions are split over the GPUs")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="rank exchange inside libcocoa_hip.so: RCCL over xGMI (one GPU per rank) or HOST (TCP)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--strict", action="store_true", help="bit-exact mode (default: fast)")
@@ -90,13 +92,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # control plane only (communicator id, barriers, max over ranks): the
+        # deltaW / objective exchange runs inside libcocoa_hip.so over RCCL
+        dist.init_process_group("gloo")
 
     import cocoa_amd  # noqa: F401
-    from cocoa_amd import configs
-    from cocoa_amd.dist import DistributedCoCoA, TorchEngine
+    from cocoa_amd import Engine, configs
+    from cocoa_amd.dist import DistributedCoCoA
 
     # ---- data: this rank's share of the seeded problem (cocoa_amd.configs) ----
     t0 = time.time()
@@ -108,22 +111,22 @@ def main():
     log(f"rank {rank}: data n={tr.n} nnz={tr.nnz} d={args.d} K_loc={tr.num_parts} K={K_glob} H={H} "
         f"gen {time.time() - t0:.1f}s")
 
-    eng = TorchEngine(device=local_rank, strict=args.strict)
+    eng = Engine(device=local_rank, strict=args.strict)
     eng.set_train(tr, part_begin=sh.part_begin, num_parts_global=K_glob)
     eng.set_test(te)
     eng.init(args.method, n_glob, 1 << 30, H, args.lam)
-    runner = DistributedCoCoA(eng)
+    runner = DistributedCoCoA(eng, transport=args.transport)
 
     def barrier():
-        torch.cuda.synchronize()
+        eng.sync()  # the engine's own HIP stream
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        eng.sync()
 
     def max_over_ranks(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -232,7 +235,9 @@ def main():
                        "method": args.method,
                        "n_total": n_glob, "K_total": K_glob, "H": H, "nnz_per_gpu": tr.nnz, "test_rows_per_gpu": te.n,
                        "mode": "strict" if args.strict else "fast",
-                       "parallelism": f"dp{world}: {tr.num_parts} partitions per GPU, deltaW all-reduce (RCCL)"},
+                       "parallelism": f"dp{world}: {tr.num_parts} partitions per GPU, deltaW "
+                                      f"{'all-reduce' if not args.strict else 'ordered chain'} inside libcocoa_hip.so "
+                                      f"({args.transport.upper()})"},
             "time_to_gap_s": ttg, "rounds_to_gap": rounds_to_gap, "gap_target": args.gap_target,
             "final_gap": final_gap, "gap_trajectory_timed": gaps,
             "roofline": {"kernel": "solver (local SDCA, CoCoA.localSDCA)", "bound": "hbm", "achieved": ach,

@@ -122,7 +122,17 @@ SIGNATURES = {
                                     ctypes.POINTER(Dataset)]),
     "cocoa_dataset_free": (None, [ctypes.POINTER(Dataset)]),
     "cocoa_jrandom_ints": (_int, [_i64, _i32, _i32, _pi32]),
+    "cocoa_comm_unique_id": (_int, [_int, ctypes.c_char_p]),
+    "cocoa_comm_init": (_int, [_vp, _int, _i32, _i32, ctypes.c_char_p]),
+    "cocoa_comm_info": (_int, [_vp, _pi32, _pi32, _pi32]),
+    "cocoa_comm_create": (_int, [_int, _i32, _i32, ctypes.c_char_p, _int, ctypes.POINTER(_vp)]),
+    "cocoa_comm_destroy": (_int, [_vp]),
+    "cocoa_comm_allreduce": (_int, [_vp, _pf64, _i64]),
+    "cocoa_comm_ordered_sum": (_int, [_vp, _pf64, _i64]),
 }
+
+TRANSPORTS = {"rccl": 0, "host": 1}
+UID_BYTES = 128
 
 _lib = None
 

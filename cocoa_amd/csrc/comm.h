@@ -52,7 +52,7 @@ struct Comm {
     // every rank gets the last rank's buffer
     void bcast_last(double* buf, int64_t n, bool device, hipStream_t s);
 
-  private:
+    // internals (also used by comm_create)
     void host_send(int fd, const void* p, size_t bytes);
     void host_recv(int fd, void* p, size_t bytes);
     double* scratch(int64_t n);

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/cocoa_capi.h"
+#include "comm.h"
 #include "common.h"
 #include "jrandom.h"
 #include "kernels.h"
@@ -85,9 +86,15 @@ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 }  // namespace
 
+struct cocoa_comm {
+    cocoa::Comm* c = nullptr;
+};
+
 struct cocoa_ctx {
     int device = 0;
     bool strict = false;
+    // rank exchange (cocoa_comm_init): owned; null = single rank / caller-driven
+    cocoa::Comm* comm = nullptr;
     hipStream_t stream = nullptr;
     bool own_stream = false;
     std::string err;
@@ -203,6 +210,7 @@ struct cocoa_ctx {
     }
     ~cocoa_ctx() {
         if (stream) (void)hipStreamSynchronize(stream);
+        delete comm;
         if (zstream) {
             (void)hipStreamSynchronize(zstream);
             (void)hipStreamDestroy(zstream);
@@ -662,7 +670,9 @@ static bool dw_double_buffer(size_t bytes) {
     return bytes >= ((size_t)1 << 30);
 }
 
-static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
+// fuse_apply: w += sum * mult inside the fold (one rank, no exchange).
+// chain_init: strict multi-rank fold, continuing the previous ranks' fold.
+static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* chain_init = nullptr) {
     require(c->inited, COCOA_E_STATE, "cocoa_round: call cocoa_init first");
     const int32_t H = c->P.local_iters;
     const int32_t seed = wrap32((int64_t)c->D.seed + t);                    // debug.seed + t
@@ -746,9 +756,10 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply) {
         c->timed(COCOA_K_APPLY, [&] { launch_scale(c->w.as<double>(), d, 1.0 - (step * c->P.lambda), s); });
         c->mult = step * c->scaling;
     }
+    if (chain_init) c->comm->chain_recv(c->dw_sum, d, true, s);  // the fold of ranks < rank (rank > 0)
     c->timed(COCOA_K_FOLD, [&] {
         launch_fold(dws, K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, c->d_inv.as<int32_t>(),
-                    !c->dw_dbuf, s);
+                    !c->dw_dbuf, s, chain_init);
     });
     if (c->dw_dbuf) c->zero_owed = set;
     c->xw_cached = false;  // w moves this round (scale / fused apply / the caller's apply)
@@ -784,9 +795,119 @@ extern "C" int cocoa_round_apply(cocoa_ctx* ctx) {
     CAPI_END(ctx)
 }
 
+// One full round.  With a communicator (cocoa_comm_init) the deltaW sum is
+// exchanged between ranks before w moves (CoCoA.scala:47-48):
+//   fast   -- allreduce of the rank-local folds (one fixed association, the
+//             same bytes on every rank);
+//   strict -- the ordered chain: rank r continues the fold of ranks < r and
+//             passes it on, the last rank broadcasts the total, so the sum is
+//             the single-process partition-order fold bit for bit.
 extern "C" int cocoa_round(cocoa_ctx* ctx, int32_t t) {
     CAPI_BEGIN(ctx)
-    run_local(ctx, t, true);
+    if (!ctx->comm) {
+        run_local(ctx, t, true);
+    } else {
+        cocoa::Comm& cm = *ctx->comm;
+        const int64_t d = ctx->d;
+        if (ctx->strict && cm.world > 1) {
+            run_local(ctx, t, false, cm.rank > 0 ? ctx->dw_sum : nullptr);
+            cm.chain_send(ctx->dw_sum, d, true, ctx->stream);
+            cm.bcast_last(ctx->dw_sum, d, true, ctx->stream);
+        } else {
+            run_local(ctx, t, false);
+            cm.allreduce(ctx->dw_sum, d, true, ctx->stream);
+        }
+        ctx->timed(COCOA_K_APPLY, [&] {
+            launch_apply(ctx->w.as<double>(), ctx->dw_sum, d, ctx->mult, ctx->d_inv.as<int32_t>(), ctx->stream);
+        });
+        ctx->xw_cached = false;
+    }
+    CAPI_END(ctx)
+}
+
+// ------------------------------------------------------------ rank exchange --
+extern "C" int cocoa_comm_unique_id(int transport, void* uid) {
+    try {
+        require(uid != nullptr, COCOA_E_ARG, "cocoa_comm_unique_id: null uid");
+        cocoa::comm_unique_id(transport, uid);
+    } catch (const Error& e) {
+        cocoa_set_global_error(e.what());
+        return e.code;
+    }
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_comm_create(int transport, int32_t rank, int32_t world, const void* uid, int device,
+                                 cocoa_comm** out) {
+    if (!out) return COCOA_E_ARG;
+    *out = nullptr;
+    try {
+        cocoa_comm* c = new cocoa_comm();
+        try {
+            c->c = cocoa::comm_create(transport, rank, world, uid, device);
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+    } catch (const Error& e) {
+        cocoa_set_global_error(e.what());
+        return e.code;
+    }
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_comm_destroy(cocoa_comm* comm) {
+    if (comm) {
+        delete comm->c;
+        delete comm;
+    }
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_comm_allreduce(cocoa_comm* comm, double* buf, int64_t n) {
+    try {
+        require(comm && comm->c && (buf || n == 0) && n >= 0, COCOA_E_ARG, "cocoa_comm_allreduce: bad argument");
+        comm->c->allreduce(buf, n, false, nullptr);
+    } catch (const Error& e) {
+        cocoa_set_global_error(e.what());
+        return e.code;
+    }
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_comm_ordered_sum(cocoa_comm* comm, double* buf, int64_t n) {
+    try {
+        require(comm && comm->c && (buf || n == 0) && n >= 0, COCOA_E_ARG, "cocoa_comm_ordered_sum: bad argument");
+        cocoa::Comm& cm = *comm->c;
+        std::vector<double> mine(buf, buf + n);
+        if (cm.rank > 0) {
+            cm.chain_recv(buf, n, false, nullptr);
+            for (int64_t i = 0; i < n; ++i) buf[i] = buf[i] + mine[(size_t)i];
+        }
+        cm.chain_send(buf, n, false, nullptr);
+        cm.bcast_last(buf, n, false, nullptr);
+    } catch (const Error& e) {
+        cocoa_set_global_error(e.what());
+        return e.code;
+    }
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_comm_init(cocoa_ctx* ctx, int transport, int32_t rank, int32_t world, const void* uid) {
+    CAPI_BEGIN(ctx)
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    delete ctx->comm;
+    ctx->comm = nullptr;
+    ctx->comm = cocoa::comm_create(transport, rank, world, uid, ctx->device);
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_comm_info(cocoa_ctx* ctx, int32_t* transport, int32_t* rank, int32_t* world) {
+    CAPI_BEGIN(ctx)
+    if (transport) *transport = ctx->comm ? ctx->comm->transport : -1;
+    if (rank) *rank = ctx->comm ? ctx->comm->rank : 0;
+    if (world) *world = ctx->comm ? ctx->comm->world : 1;
     CAPI_END(ctx)
 }
 
@@ -847,7 +968,46 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     });
     HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    finish(ctx, ctx->h_eval[0], ctx->h_eval[1], ctx->h_eval[2], (int64_t)ctx->h_eval[3], e.n_test, out);
+    double hinge = ctx->h_eval[0], alpha_sum = ctx->h_eval[1];
+    const double w2 = ctx->h_eval[2];  // w is replicated: the same on every rank
+    double counts[2] = {ctx->h_eval[3], (double)e.n_test};
+    if (ctx->comm && ctx->comm->world > 1) {
+        cocoa::Comm& cm = *ctx->comm;
+        if (ctx->strict) {
+            // continue the partition-order merge of the previous ranks
+            // (OptUtils.scala:65-84 as Spark merges partitions, in index order):
+            // carry = {hinge, hinge-seen flag, alpha}
+            std::vector<double> part((size_t)2 * ctx->K_loc);
+            HIPCHK(hipMemcpyAsync(part.data(), ctx->eval_part.p, sizeof(double) * part.size(), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            double carry[3] = {0.0, 0.0, 0.0};
+            cm.chain_recv(carry, 3, false, ctx->stream);
+            bool have = carry[1] != 0.0;
+            double h = carry[0], al = carry[2];
+            for (int32_t k = 0; k < ctx->K_loc; ++k) {
+                al = (cm.rank == 0 && k == 0) ? part[2 * (size_t)k + 1] : al + part[2 * (size_t)k + 1];
+                if (ctx->h_part_ptr[(size_t)k + 1] > ctx->h_part_ptr[(size_t)k]) {
+                    h = have ? h + part[2 * (size_t)k] : part[2 * (size_t)k];
+                    have = true;
+                }
+            }
+            carry[0] = h;
+            carry[1] = have ? 1.0 : 0.0;
+            carry[2] = al;
+            cm.chain_send(carry, 3, false, ctx->stream);
+            cm.bcast_last(carry, 3, false, ctx->stream);
+            hinge = carry[0];
+            alpha_sum = carry[2];
+        } else {
+            double sums[2] = {hinge, alpha_sum};
+            cm.allreduce(sums, 2, false, ctx->stream);
+            hinge = sums[0];
+            alpha_sum = sums[1];
+        }
+        cm.allreduce(counts, 2, false, ctx->stream);  // integers: exact in any order
+    }
+    finish(ctx, hinge, alpha_sum, w2, (int64_t)counts[0], (int64_t)counts[1], out);
     CAPI_END(ctx)
 }
 

@@ -154,7 +154,7 @@ void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H,
 // original order, the order ranks exchange it in
 void launch_zero(double* p, int64_t n, int blocks, hipStream_t s);
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
-                 const int32_t* inv, bool zero, hipStream_t s);
+                 const int32_t* inv, bool zero, hipStream_t s, const double* init = nullptr);
 void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const int32_t* inv, hipStream_t s);
 void launch_scale(double* w, int64_t d, double scale, hipStream_t s);
 void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, double* out, hipStream_t s);

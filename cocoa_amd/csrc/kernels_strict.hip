@@ -64,12 +64,16 @@ void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H,
 // ------------------------------------------------------- deltaW fold/apply --
 // sum = ((dW_0 + dW_1) + dW_2) + ... in partition order (the reference's
 // reduce(_ + _), CoCoA.scala:47), zeroing each private slice for the next
-// round; then w += sum * mult (CoCoA.scala:48) or the sum is stored for an
-// external all-reduce.
+// round; then w += sum * mult (CoCoA.scala:48) or the sum is stored for the
+// exchange between ranks.  init (original feature order, or null): the fold
+// of the previous ranks' partitions, which this rank's fold continues (the
+// strict-mode chain across ranks keeps the single-process fold order).
 __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_t d, double* dw_sum, double* w,
-                                                   double mult, int apply, const int32_t* inv, int zero) {
+                                                   double mult, int apply, const int32_t* inv, int zero,
+                                                   const double* init) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
-        double s = dw[j];
+        const int64_t jo = inv ? inv[j] : j;
+        double s = init ? init[jo] + dw[j] : dw[j];
         if (zero) dw[j] = 0.0;
         for (int32_t k = 1; k < K; ++k) {
             const size_t o = (size_t)k * d + j;
@@ -79,15 +83,16 @@ __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_
         if (apply)
             w[j] = w[j] + (s * mult);
         else
-            dw_sum[inv ? inv[j] : j] = s;
+            dw_sum[jo] = s;
     }
 }
 
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
-                 const int32_t* inv, bool zero, hipStream_t s) {
+                 const int32_t* inv, bool zero, hipStream_t s, const double* init) {
     int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
     if (blocks < 1) blocks = 1;
-    fold_kernel<<<blocks, 256, 0, s>>>(const_cast<double*>(dw), K, d, dw_sum, w, mult, apply ? 1 : 0, inv, zero ? 1 : 0);
+    fold_kernel<<<blocks, 256, 0, s>>>(const_cast<double*>(dw), K, d, dw_sum, w, mult, apply ? 1 : 0, inv,
+                                       zero ? 1 : 0, init);
 }
 
 // Background re-zeroing of a folded deltaW set (double-buffered slices): a

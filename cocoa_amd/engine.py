@@ -9,6 +9,46 @@ import numpy as np
 from . import _capi as C
 
 
+def comm_unique_id(transport="rccl"):
+    """cocoa_comm_unique_id: made once on rank 0, then handed to every rank
+    (HOST opens rank 0's listening socket in this process)."""
+    buf = ctypes.create_string_buffer(C.UID_BYTES)
+    C.check(C.lib().cocoa_comm_unique_id(C.TRANSPORTS[transport], buf))
+    return buf.raw
+
+
+class Comm:
+    """Stand-alone communicator on host buffers (cocoa_comm_create): the two
+    reductions the engine uses between ranks, without a context or a GPU for
+    the HOST transport."""
+
+    def __init__(self, transport, rank, world, uid, device=-1):
+        h = ctypes.c_void_p()
+        C.check(C.lib().cocoa_comm_create(C.TRANSPORTS[transport], rank, world, uid, device, ctypes.byref(h)))
+        self.h = h
+
+    def allreduce(self, x):
+        x = np.ascontiguousarray(x, np.float64).copy()
+        C.check(C.lib().cocoa_comm_allreduce(self.h, C.f64p(x), len(x)))
+        return x
+
+    def ordered_sum(self, x):
+        x = np.ascontiguousarray(x, np.float64).copy()
+        C.check(C.lib().cocoa_comm_ordered_sum(self.h, C.f64p(x), len(x)))
+        return x
+
+    def close(self):
+        if getattr(self, "h", None):
+            C.lib().cocoa_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     def __init__(self, device=0, strict=False, stream=None):
         """stream: a hipStream_t handle as int (e.g. torch.cuda.current_stream().cuda_stream)."""
@@ -36,6 +76,18 @@ class Engine:
         data = data.contiguous()
         C.check(C.lib().cocoa_set_test(self.h, C.i64p(data.row_ptr), C.i32p(data.col), C.f64p(data.val),
                                        C.f64p(data.y), data.n), self.h)
+
+    # -- ranks ---------------------------------------------------------------
+    def comm_init(self, transport, rank, world, uid):
+        """Attach a communicator (cocoa_comm_init): round / eval / run then
+        exchange deltaW and the objective sums between the ranks internally."""
+        C.check(C.lib().cocoa_comm_init(self.h, C.TRANSPORTS[transport], rank, world, uid), self.h)
+
+    def comm_info(self):
+        t, r, w = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        C.check(C.lib().cocoa_comm_info(self.h, ctypes.byref(t), ctypes.byref(r), ctypes.byref(w)), self.h)
+        names = {v: k for k, v in C.TRANSPORTS.items()}
+        return {"transport": names.get(t.value), "rank": r.value, "world": w.value}
 
     # -- solver --------------------------------------------------------------
     def init(self, method, n, num_rounds, local_iters, lam, beta=1.0, gamma=1.0, debug_iter=10, seed=0,

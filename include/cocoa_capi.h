@@ -13,11 +13,14 @@
  *
  * Ownership: the caller owns every host buffer it passes; the engine copies
  * inputs to device memory and copies results out.  A context owns its device
- * memory and runs on one HIP device and one HIP stream; it is not thread-safe
- * and is driven from one host thread.  Multi-GPU = one process (and one
- * context) per GPU; the per-round deltaW exchange is done by the caller
- * (RCCL via torch.distributed in cocoa_amd.dist) between
- * cocoa_round_local() and cocoa_round_apply().
+ * memory, its HIP stream and its communicator; it is not thread-safe and is
+ * driven from one host thread.  Multi-GPU = one process (and one context) per
+ * GPU: rank 0 makes a communicator id (cocoa_comm_unique_id), the caller hands
+ * the 128 bytes to every rank by any means (a file, its own RPC, MPI, ...),
+ * every rank calls cocoa_comm_init, and from then on cocoa_round /
+ * cocoa_eval / cocoa_run exchange deltaW and the objective sums internally
+ * (RCCL over xGMI).  cocoa_round_local() / cocoa_round_apply() remain for a
+ * caller that does the exchange itself.
  */
 #ifndef COCOA_CAPI_H
 #define COCOA_CAPI_H
@@ -29,7 +32,7 @@
 extern "C" {
 #endif
 
-#define COCOA_CAPI_VERSION 1
+#define COCOA_CAPI_VERSION 2
 
 /* error codes */
 #define COCOA_OK 0
@@ -93,6 +96,37 @@ int cocoa_create(int device, int strict, void *stream, cocoa_ctx **out);
 int cocoa_destroy(cocoa_ctx *ctx);
 const char *cocoa_last_error(const cocoa_ctx *ctx);
 int cocoa_version(void);
+
+/* ---- rank exchange (CoCoA.scala:45-48, OptUtils.scala:65-98) ------------ */
+/* The reference sums the K partitions' deltaW with `updates.map(_._1)
+ * .reduce(_ + _)` and reduces the objective terms with RDD reduces; here the
+ * ranks exchange them directly.  Transports:
+ *   RCCL -- over xGMI, one GPU per rank (the production path);
+ *   HOST -- TCP through rank 0 (COCOA_COMM_ADDR, default 127.0.0.1), buffers
+ *           staged in host memory: ranks sharing a GPU, CPU-only use.
+ * With a communicator, fast mode allreduces the rank-local folds (one fixed
+ * association, identical bytes on every rank); strict mode passes the running
+ * partition-order fold from rank to rank (rank r continues ranks < r) and the
+ * last rank broadcasts it, so strict multi-rank runs stay bitwise equal to
+ * the single-process reference order. */
+#define COCOA_TRANSPORT_RCCL 0
+#define COCOA_TRANSPORT_HOST 1
+#define COCOA_COMM_UID_BYTES 128
+typedef struct cocoa_comm cocoa_comm;
+/* Made once, on rank 0 (HOST: opens rank 0's listening socket in this process). */
+int cocoa_comm_unique_id(int transport, void *uid /* COCOA_COMM_UID_BYTES */);
+/* Attach a communicator to the context (owned by it; replaces any previous). */
+int cocoa_comm_init(cocoa_ctx *ctx, int transport, int32_t rank, int32_t world, const void *uid);
+/* transport (-1 = none), rank and world of the context's communicator. */
+int cocoa_comm_info(cocoa_ctx *ctx, int32_t *transport, int32_t *rank, int32_t *world);
+/* Stand-alone communicator on host buffers (no context; device < 0 = none,
+ * RCCL needs one): the two reductions the engine uses. */
+int cocoa_comm_create(int transport, int32_t rank, int32_t world, const void *uid, int device, cocoa_comm **out);
+int cocoa_comm_destroy(cocoa_comm *comm);
+/* in place: buf = sum over ranks (HOST: ((x_0 + x_1) + x_2) + ... at rank 0). */
+int cocoa_comm_allreduce(cocoa_comm *comm, double *buf, int64_t n);
+/* in place: buf = ((x_0 + x_1) + ...) formed rank to rank, the strict chain. */
+int cocoa_comm_ordered_sum(cocoa_comm *comm, double *buf, int64_t n);
 
 /* ---- data (OptUtils.loadLIBSVMData result, OptUtils.scala:11-53) -------- */
 /* This rank's partitions of the training set as one CSR: rows are

@@ -1,8 +1,9 @@
-"""N>1 path on CPU: two gloo ranks run cocoa_amd.dist.DistributedCoCoA (the
-product's multi-GPU orchestration: contiguous partition shards, ordered local
-fold, all-reduce of the deltaW sum, identical w update on every rank, scalar
-all-reduce for the objectives).  The per-rank compute is the oracle here (this
-test has no GPU); the result must equal a single-process oracle run up to the
+"""N>1 path on CPU: two ranks (a gloo group for the launcher's id exchange)
+run the multi-rank round structure -- contiguous partition shards, ordered
+local fold, the library's rank exchange (cocoa_comm_allreduce, HOST
+transport) of the deltaW sum, identical w update on every rank, exchange of
+the objective sums.  The per-rank compute is the oracle here (this test has
+no GPU); the result must equal a single-process oracle run up to the
 re-association of the cross-rank sum."""
 import os
 import socket
@@ -14,14 +15,17 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from cocoa_amd.data import load_libsvm
-from cocoa_amd.dist import DistributedCoCoA, shard_bounds
+from cocoa_amd.dist import shard_bounds
+from cocoa_amd.engine import Comm, comm_unique_id
 from oracle import oracle
 
 G = os.path.join(os.path.dirname(__file__), "golden", "data")
 
 
 class OracleEngine:
-    """Implements the engine interface DistributedCoCoA drives, on the oracle."""
+    """One rank of the multi-rank round (cocoa_round with a communicator), with
+    the oracle doing the rank-local compute and the library's HOST-transport
+    communicator doing the exchange."""
 
     def __init__(self, shard, test_shard, method, n, H, lam, Kg):
         self.data = oracle.Data(shard.row_ptr, shard.col, shard.val, shard.y, shard.part_ptr, shard.num_features)
@@ -30,15 +34,12 @@ class OracleEngine:
         self.run = oracle.Run(self.data, method, n, H, lam)
         self.run.set_global_parts(Kg)
         self.n, self.lam = n, lam
-        self.dw_sum = torch.zeros(shard.num_features, dtype=torch.float64)
+        self.comm = None
 
-    def round_local(self, t):
+    def round(self, t):
         buf = np.zeros(self.data.d)
         self.run.round_local(t, buf)
-        self.dw_sum.copy_(torch.from_numpy(buf))
-
-    def round_apply(self):
-        self.run.round_apply(self.dw_sum.numpy())
+        self.run.round_apply(self.comm.allreduce(buf))
 
     def eval(self):
         ev = self.run.eval(self.test)
@@ -46,8 +47,8 @@ class OracleEngine:
         w2 = 0.0
         for x in w:
             w2 += x * x
-        return {"hinge_sum": ev["hinge_sum"], "alpha_sum": ev["alpha_sum"], "w_sqnorm": w2,
-                "test_err_count": ev["test_err"], "test_rows": self.test.n}
+        h, a, e, r = self.comm.allreduce([ev["hinge_sum"], ev["alpha_sum"], ev["test_err"], self.test.n])
+        return self.eval_finish(h, a, w2, e, r)
 
     def eval_finish(self, h, a, w2, e, r):
         nw = np.sqrt(w2)
@@ -64,12 +65,14 @@ def _worker(rank, world, port, method, T, q):
     k0, k1 = shard_bounds(4, world, rank)
     r0, r1 = shard_bounds(te.n, world, rank)
     eng = OracleEngine(tr.shard(k0, k1), te.row_range(r0, r1), method, tr.n, 50, 1e-3, 4)
-    runner = DistributedCoCoA(eng)
+    obj = [comm_unique_id("host") if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)   # the launcher's job (cocoa_amd.dist)
+    eng.comm = Comm("host", rank, world, obj[0])
     evs = []
     for t in range(1, T + 1):
-        runner.round(t)
+        eng.round(t)
         if t % 5 == 0:
-            evs.append(runner.eval())
+            evs.append(eng.eval())
     q.put((rank, eng.run.w(), eng.run.alpha(), evs))
     dist.barrier()
     dist.destroy_process_group()

@@ -1,0 +1,159 @@
+"""Multi-rank runs through the C ABI's own exchange (cocoa_comm_init): no torch
+collective in the data path, exactly what a JVM caller over FFM would drive.
+
+* world 1 over RCCL: cocoa_round / cocoa_eval take the communicator path
+  (fold -> ncclAllReduce / chain -> apply) and must give the golden C1
+  results bit for bit, as the fused single-rank path does;
+* 2 and 4 processes sharing the box's one GPU over the HOST transport (RCCL
+  refuses two ranks on one device): contiguous partition blocks per rank
+  (CoCoA.scala:28), deltaW exchanged every round (CoCoA.scala:47-48), the
+  objective sums every evaluation (OptUtils.scala:65-98).  Strict mode passes
+  the partition-order fold from rank to rank, so it must equal the
+  single-process oracle bit for bit; fast mode (allreduce) within 1e-9.
+"""
+import json
+import multiprocessing as mp
+import os
+
+import numpy as np
+import pytest
+
+import cocoa_amd
+from cocoa_amd import Engine
+from cocoa_amd.configs import shard_bounds
+from cocoa_amd.engine import comm_unique_id
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+TRAIN = os.path.join(G, "data", "small_train.dat")
+TEST = os.path.join(G, "data", "small_test.dat")
+METHODS = ["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"]
+T, H, LAM = 12, 50, 1e-3
+
+
+def _j(name):
+    return json.load(open(os.path.join(G, name)))
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_world1_rccl_comm_path_is_bitwise_golden(method):
+    tr, te = cocoa_amd.load_libsvm(TRAIN, 4, 9947), cocoa_amd.load_libsvm(TEST, 4, 9947)
+    fx = _j("c1_%s.json" % method.replace("+", "plus"))
+    cfg = _j("c1_meta.json")["config"]
+    e = Engine(strict=True)
+    e.set_train(tr)
+    e.set_test(te)
+    e.comm_init("rccl", 0, 1, comm_unique_id("rccl"))
+    assert e.comm_info() == {"transport": "rccl", "rank": 0, "world": 1}
+    e.init(method, tr.n, cfg["T"], cfg["H"], cfg["lam"], cfg["beta"], cfg["gamma"], cfg["debug_iter"], cfg["seed"])
+    recs = {r["t"]: r for r in fx["trace"]}
+    for t in range(1, cfg["T"] + 1):
+        e.round(t)
+        if t in recs:
+            ev = e.eval()
+            assert ev["primal"].hex() == recs[t]["primal"], t
+            assert ev["test_err_count"] == recs[t]["test_err"], t
+    import hashlib
+    assert hashlib.sha256(np.ascontiguousarray(e.w(), "<f8").tobytes()).hexdigest() == fx["w_sha256"]
+
+
+def _rank_worker(rank, world, strict, methods, uid_q, out_q):
+    try:
+        tr = cocoa_amd.load_libsvm(TRAIN, 4, 9947)
+        te = cocoa_amd.load_libsvm(TEST, 4, 9947)
+        k0, k1 = shard_bounds(4, world, rank)
+        r0, r1 = shard_bounds(te.n, world, rank)
+        if rank == 0:
+            uid = comm_unique_id("host")
+            for _ in range(world - 1):
+                uid_q.put(uid)
+        else:
+            uid = uid_q.get(timeout=60)
+        e = Engine(device=0, strict=strict)
+        e.set_train(tr.shard(k0, k1), part_begin=k0, num_parts_global=4)
+        e.set_test(te.row_range(r0, r1))
+        e.comm_init("host", rank, world, uid)
+        res = {}
+        for m in methods:
+            e.init(m, tr.n, T, H, LAM, 1.0, 1.0, 4, 0)
+            evs = []
+            for t in range(1, T + 1):
+                e.round(t)
+                if t % 4 == 0:
+                    evs.append(e.eval())
+            res[m] = (e.w(), e.alpha(), evs)
+        # cocoa_run drives the same exchange (the FFM / JNI caller's entry point)
+        seen = []
+        e.run("cocoa+", tr.n, 8, H, LAM, debug_iter=4, callback=lambda t, ev: seen.append((t, ev)))
+        res["run"] = (e.w(), seen)
+        e.close()
+        out_q.put((rank, res))
+    except Exception as ex:
+        out_q.put((rank, repr(ex)))
+
+
+def _spawn(world, strict, methods):
+    ctx = mp.get_context("spawn")
+    uid_q, out_q = ctx.Queue(), ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, strict, methods, uid_q, out_q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = dict(out_q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert not isinstance(out[r], str), out[r]
+    return out
+
+
+def _oracle(method, Tr=T):
+    od = oracle.Data.load_libsvm(TRAIN, 4, 9947)
+    ot = oracle.Data.load_libsvm(TEST, 4, 9947)
+    run = oracle.Run(od, method, od.n, H, LAM)
+    evs = []
+    for t in range(1, Tr + 1):
+        run.round(t)
+        if t % 4 == 0:
+            evs.append(run.eval(ot))
+    return run, evs
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_multirank_strict_chain_is_bitwise_single_process(world):
+    out = _spawn(world, True, METHODS)
+    for m in METHODS:
+        run, revs = _oracle(m)
+        w_ref = run.w()
+        for r in range(world):
+            assert out[r][m][0].tobytes() == w_ref.tobytes(), (m, r)          # identical bytes on every rank
+        if m in ("cocoa+", "cocoa", "mbcd"):
+            a = np.concatenate([out[r][m][1] for r in range(world)])
+            assert a.tobytes() == run.alpha().tobytes(), m
+        for ev, rv in zip(out[0][m][2], revs):
+            assert ev["primal"].hex() == rv["primal"].hex(), m
+            if m in ("cocoa+", "cocoa", "mbcd"):
+                assert ev["gap"].hex() == rv["gap"].hex(), m
+            assert ev["test_err_count"] == rv["test_err"] and ev["test_rows"] == 600
+    run, revs = _oracle("cocoa+", 8)
+    assert out[0]["run"][0].tobytes() == run.w().tobytes()
+    assert [t for t, _ in out[0]["run"][1]] == [4, 8]
+    assert [ev["gap"].hex() for _, ev in out[0]["run"][1]] == [rv["gap"].hex() for rv in revs]
+
+
+def test_multirank_fast_allreduce_within_tolerance():
+    world = 2
+    out = _spawn(world, False, ["cocoa+", "mbcd", "mbsgd"])
+    for m in ("cocoa+", "mbcd", "mbsgd"):
+        run, revs = _oracle(m)
+        w_ref = run.w()
+        assert out[0][m][0].tobytes() == out[1][m][0].tobytes()                # allreduce: same bytes
+        assert np.max(np.abs(out[0][m][0] - w_ref)) <= 1e-9 * np.max(np.abs(w_ref))
+        for ev, rv in zip(out[0][m][2], revs):
+            assert abs(ev["primal"] - rv["primal"]) <= 1e-9 * abs(rv["primal"])
+            assert ev["test_err_count"] == rv["test_err"]
