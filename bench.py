@@ -111,7 +111,10 @@ def main():
     log(f"rank {rank}: data n={tr.n} nnz={tr.nnz} d={args.d} K_loc={tr.num_parts} K={K_glob} H={H} "
         f"gen {time.time() - t0:.1f}s")
 
-    eng = Engine(device=local_rank, strict=args.strict)
+    # one GPU per rank; ranks beyond the visible devices share them (HOST
+    # transport rehearsals on a one-GPU box -- RCCL needs distinct GPUs)
+    ndev = max(torch.cuda.device_count(), 1)
+    eng = Engine(device=local_rank % ndev, strict=args.strict)
     eng.set_train(tr, part_begin=sh.part_begin, num_parts_global=K_glob)
     eng.set_test(te)
     eng.init(args.method, n_glob, 1 << 30, H, args.lam)
