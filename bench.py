@@ -64,6 +64,8 @@ def main():
                          "(n rows, K = parts) whose partitions are split over the GPUs")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="rank exchange inside libcocoa_hip.so: RCCL over xGMI (one GPU per rank) or HOST (TCP)")
+    ap.add_argument("--solver", default="auto", choices=["auto", "gram", "chain"],
+                    help="fast-mode SDCA local solver (cocoa_set_solver)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--strict", action="store_true", help="bit-exact mode (default: fast)")
@@ -116,6 +118,7 @@ def main():
     ndev = max(torch.cuda.device_count(), 1)
     eng = Engine(device=local_rank % ndev, strict=args.strict)
     eng.set_train(tr, part_begin=sh.part_begin, num_parts_global=K_glob)
+    eng.set_solver(args.solver)
     eng.set_test(te)
     eng.init(args.method, n_glob, 1 << 30, H, args.lam)
     runner = DistributedCoCoA(eng, transport=args.transport)

@@ -18,8 +18,9 @@ E_ARG, E_PARSE, E_RANGE, E_IO, E_HIP, E_STATE, E_NODEV = -1, -2, -3, -4, -5, -6,
 
 METHOD_COCOA_PLUS, METHOD_COCOA, METHOD_MBCD, METHOD_MBSGD, METHOD_LOCALSGD = 0, 1, 2, 3, 4
 METHODS = {"cocoa+": 0, "cocoa": 1, "mbcd": 2, "mbsgd": 3, "localsgd": 4}
-K_SAMPLE, K_SOLVER, K_FOLD, K_APPLY, K_EVAL, K_PLAN = 0, 1, 2, 3, 4, 5
-KERNEL_NAMES = ["sample", "solver", "fold", "apply", "eval", "plan"]
+K_SAMPLE, K_SOLVER, K_FOLD, K_APPLY, K_EVAL, K_PLAN, K_GRAM = 0, 1, 2, 3, 4, 5, 6
+KERNEL_NAMES = ["sample", "solver", "fold", "apply", "eval", "plan", "gram"]
+SOLVERS = {"auto": 0, "chain": 1, "gram": 2}
 
 
 class CocoaError(RuntimeError):
@@ -122,6 +123,7 @@ SIGNATURES = {
                                     ctypes.POINTER(Dataset)]),
     "cocoa_dataset_free": (None, [ctypes.POINTER(Dataset)]),
     "cocoa_jrandom_ints": (_int, [_i64, _i32, _i32, _pi32]),
+    "cocoa_set_solver": (_int, [_vp, _int]),
     "cocoa_comm_unique_id": (_int, [_int, ctypes.c_char_p]),
     "cocoa_comm_init": (_int, [_vp, _int, _i32, _i32, ctypes.c_char_p]),
     "cocoa_comm_info": (_int, [_vp, _pi32, _pi32, _pi32]),

@@ -153,6 +153,11 @@ struct cocoa_ctx {
     size_t lds_bytes = 0;
     SolverArgs sa{};
     bool use_plan = false;
+    // Gram-window solver (fast SDCA methods on sparse rows, solver_gram.h)
+    int solver_kind = COCOA_SOLVER_AUTO;
+    bool use_gram = false;
+    DevBuf gt, status;  // status: set by a Gram-solver launch whose hand-off timed out
+    int32_t nbatch = 0;
     DevBuf plan_beg, plan_z, plan_y, plan_q, plan_xw;
     // x.w of every train row for the current w, written by the fast eval pass
     // (eval v4) and reused by the next round's plan; false once w moves
@@ -250,6 +255,14 @@ struct cocoa_ctx {
 
 static void require(bool cond, int code, const std::string& msg) {
     if (!cond) throw Error(code, msg);
+}
+
+// after a stream synchronisation: a Gram-solver launch that had to abort
+static void check_status(cocoa_ctx* c) {
+    if (!c->use_gram || !c->status.p) return;
+    int st = 0;
+    HIPCHK(hipMemcpy(&st, c->status.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (st) throw Error(COCOA_E_HIP, "local solver: a hand-off between the solver's waves timed out (launch aborted)");
 }
 
 // ---------------------------------------------------------------- context --
@@ -535,6 +548,15 @@ static int reg_chunks_for(int64_t nnz, int64_t rows, int method) {
 
 static bool dw_double_buffer(size_t bytes);
 
+extern "C" int cocoa_set_solver(cocoa_ctx* ctx, int kind) {
+    CAPI_BEGIN(ctx)
+    require(kind == COCOA_SOLVER_AUTO || kind == COCOA_SOLVER_CHAIN || kind == COCOA_SOLVER_GRAM, COCOA_E_ARG,
+            "cocoa_set_solver: unknown solver");
+    ctx->solver_kind = kind;
+    ctx->inited = false;  // takes effect at the next cocoa_init
+    CAPI_END(ctx)
+}
+
 extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
                           const double* w_init) {
     CAPI_BEGIN(ctx)
@@ -633,6 +655,21 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
 
     // the loader of the SDCA solvers is fed by the per-step plan
     ctx->use_plan = is_sdca(method);
+    // fast SDCA: the Gram-window solver, unless the rows are dense-long (C3:
+    // 2,000 entries per row, where the chain solver streams w / deltaW from LDS)
+    const double zavg = ctx->tr.n ? (double)ctx->tr.nnz / (double)ctx->tr.n : 0.0;
+    ctx->use_gram = !ctx->strict && is_sdca(method) && H >= 1 &&
+                    (ctx->solver_kind == COCOA_SOLVER_GRAM || (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0));
+    if (ctx->use_gram) {
+        ctx->status.alloc_zero(sizeof(int) * 4, s);
+        ctx->nbatch = (H + 31) / 32;
+        if (method != COCOA_METHOD_MBCD)
+            ctx->gt.alloc(sizeof(double) * (size_t)K * (size_t)ctx->nbatch * 32 * 64);
+        else
+            ctx->gt.free();
+    } else {
+        ctx->gt.free();
+    }
     a.plan_beg = nullptr;
     a.plan_z = nullptr;
     a.plan_y = a.plan_q = a.plan_xw = nullptr;
@@ -714,7 +751,9 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             pa.w = c->w.as<double>();
             pa.steps = (int64_t)K * H;
             pa.H = H;
-            pa.need_xw = c->method != COCOA_METHOD_COCOA;  // CoCoA's w moves inside the round
+            // CoCoA's w moves inside the round: the chain solver forms x.w itself;
+            // the Gram solver splits x.w_local = x.w + x.deltaW
+            pa.need_xw = c->method != COCOA_METHOD_COCOA || c->use_gram;
             pa.xw_cache = (c->xw_cached && !c->strict) ? c->row_xw.as<double>() : nullptr;
             pa.beg = c->plan_beg.as<int64_t>();
             pa.z = c->plan_z.as<int32_t>();
@@ -728,7 +767,45 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
                     launch_plan_fast(pa, s);
             });
         }
-        if (is_sdca(c->method)) {
+        if (c->use_gram) {
+            if (c->method != COCOA_METHOD_MBCD) {
+                GramArgs ga{};
+                ga.part_ptr = c->part_ptr.as<int64_t>();
+                ga.samples = c->samples.as<int32_t>();
+                ga.row_ptr = c->tr.row_ptr.as<int64_t>();
+                ga.col = c->tr.col.as<int32_t>();
+                ga.val = c->tr.val.as<double>();
+                ga.K = K;
+                ga.H = H;
+                ga.nbatch = c->nbatch;
+                ga.gt = c->gt.as<double>();
+                c->timed(COCOA_K_GRAM, [&] { launch_gram(ga, s); });
+            }
+            GramSolverArgs g{};
+            g.part_ptr = c->part_ptr.as<int64_t>();
+            g.samples = c->samples.as<int32_t>();
+            g.plan_beg = c->plan_beg.as<int64_t>();
+            g.plan_z = c->plan_z.as<int32_t>();
+            g.plan_y = c->plan_y.as<double>();
+            g.plan_q = c->plan_q.as<double>();
+            g.plan_xw = c->plan_xw.as<double>();
+            g.col = c->tr.col.as<int32_t>();
+            g.val = c->tr.val.as<double>();
+            g.alpha = c->alpha.as<double>();
+            g.alpha_work = c->alpha_work.as<double>();
+            g.dw = dws;
+            g.gt = c->gt.p ? c->gt.as<double>() : nullptr;
+            g.status = c->status.as<int>();
+            g.d = d;
+            g.H = H;
+            g.nbatch = c->nbatch;
+            g.raw_alpha = 0;
+            g.lam_n = c->sa.lam_n;
+            g.inv_lam_n = 1.0 / c->sa.lam_n;
+            g.sigma = c->method == COCOA_METHOD_COCOA_PLUS ? c->sa.sigma : 1.0;
+            g.scaling = c->scaling;
+            c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(solver_mode(c->method), g, K, c->max_nl, s); });
+        } else if (is_sdca(c->method)) {
             c->timed(COCOA_K_SOLVER, [&] {
                 if (c->strict)
                     launch_solver_strict(solver_mode(c->method), c->vec_lds, c->alpha_lds, c->sa, K, c->lds_bytes, s);
@@ -968,6 +1045,7 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     });
     HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    check_status(ctx);
     double hinge = ctx->h_eval[0], alpha_sum = ctx->h_eval[1];
     const double w2 = ctx->h_eval[2];  // w is replicated: the same on every rank
     double counts[2] = {ctx->h_eval[3], (double)e.n_test};
@@ -1101,6 +1179,7 @@ extern "C" int cocoa_resume(cocoa_ctx* ctx, const cocoa_params* params, const co
 extern "C" int cocoa_sync(cocoa_ctx* ctx) {
     CAPI_BEGIN(ctx)
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    check_status(ctx);
     CAPI_END(ctx)
 }
 
@@ -1416,10 +1495,10 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
     std::snprintf(buf, (size_t)len,
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
-                  "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d}",
+                  "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\"}",
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,
-                  ctx->dw_dbuf ? 1 : 0);
+                  ctx->dw_dbuf ? 1 : 0, ctx->use_gram ? "gram" : "chain");
     CAPI_END(ctx)
 }

@@ -102,6 +102,42 @@ struct PlanArgs {
     double* xw;
 };
 
+// Gram-window local solver (solver_gram.h), fast mode
+struct GramArgs {
+    const int64_t* part_ptr;
+    const int32_t* samples;   // K_loc * H
+    const int64_t* row_ptr;
+    const int32_t* col;
+    const double* val;
+    int32_t K, H, nbatch;     // nbatch = ceil(H / 32)
+    int32_t pad;
+    double* gt;               // [K][nbatch * 32][64]
+};
+
+struct GramSolverArgs {
+    const int64_t* part_ptr;
+    const int32_t* samples;
+    const int64_t* plan_beg;
+    const int32_t* plan_z;
+    const double* plan_y;
+    const double* plan_q;
+    const double* plan_xw;
+    const int32_t* col;
+    const double* val;
+    double* alpha;            // alphaOld (persistent)
+    double* alpha_work;       // working alpha when it does not fit in LDS
+    double* dw;               // K_loc * d private deltaW (zero on entry)
+    const double* gt;         // Gram rows of the round (gram_kernel)
+    int* status;              // set to 1 if a hand-off wait timed out (the launch then drains)
+    int64_t d;
+    int32_t H, nbatch;
+    int32_t raw_alpha;
+    int32_t pad;
+    double lam_n, inv_lam_n;
+    double sigma;             // sigma' = K gamma (CoCoA+)
+    double scaling;
+};
+
 struct EvalArgs {
     // train side
     const int64_t* row_ptr;
@@ -142,6 +178,11 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
 int eval_fast_blocks(int64_t n, int64_t n_test);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
+// Gram-window solver: lds bytes for a partition of max_nl rows (alpha in LDS
+// when it fits, else in alpha_work)
+size_t gram_solver_lds(int32_t max_nl, bool* alv_lds);
+void launch_gram(const GramArgs& a, hipStream_t s);
+void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, int32_t max_nl, hipStream_t s);
 
 // strict translation unit
 void launch_plan_strict(const PlanArgs& a, hipStream_t s);

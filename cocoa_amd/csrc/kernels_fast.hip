@@ -5,6 +5,7 @@
 
 #include "kernels.h"
 #include "plan_impl.h"
+#include "solver_gram.h"
 #include "solver_impl.h"
 #include "wave.h"
 
@@ -16,6 +17,47 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
 }
 
 void launch_plan_fast(const PlanArgs& a, hipStream_t s) { launch_plan_impl<false>(a, s); }
+
+// ------------------------------------------------- Gram-window solver --
+size_t gram_solver_lds(int32_t max_nl, bool* alv_lds) {
+    const size_t base = (sizeof(GramSolverLds) + 15) & ~(size_t)15;
+    const size_t al = sizeof(double) * (size_t)(max_nl > 0 ? max_nl : 1);
+    const bool fits = base + al <= 160 * 1024;
+    if (alv_lds) *alv_lds = fits;
+    return fits ? base + al : base;
+}
+
+void launch_gram(const GramArgs& a, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(GramLds));
+        attr = true;
+    }
+    const int64_t grid = (int64_t)a.K * a.nbatch;
+    if (grid > 0) gram_kernel<<<(unsigned)grid, 256, sizeof(GramLds), s>>>(a);
+}
+
+template <int MODE, bool ALV>
+static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
+    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, ALV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    solver_gram_kernel<MODE, ALV><<<grid, 256, lds, s>>>(a);
+}
+
+void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, int32_t max_nl, hipStream_t s) {
+    bool alv = false;
+    const size_t lds = gram_solver_lds(max_nl, &alv);
+#define COCOA_SG(M)                        \
+    do {                                   \
+        if (alv) launch_sg<M, true>(a, grid, lds, s);  \
+        else launch_sg<M, false>(a, grid, lds, s);     \
+    } while (0)
+    if (mode == MODE_PLUS) COCOA_SG(MODE_PLUS);
+    else if (mode == MODE_COCOA) COCOA_SG(MODE_COCOA);
+    else COCOA_SG(MODE_MBCD);
+#undef COCOA_SG
+}
 
 // ----------------------------------------------------------- fused eval --
 // One pass over train + test CSR (OptUtils.scala:57-98) as a CSR stream.

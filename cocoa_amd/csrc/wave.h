@@ -25,6 +25,12 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
     return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
 }
 
+__device__ __forceinline__ int64_t readlane_i64(int64_t x, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)x, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)((uint64_t)x >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 // Move a double through DPP (both 32-bit halves with the same control).
 // Lanes whose source is disabled / out of row receive +0.0.
 template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>

@@ -90,6 +90,10 @@ class Engine:
         return {"transport": names.get(t.value), "rank": r.value, "world": w.value}
 
     # -- solver --------------------------------------------------------------
+    def set_solver(self, kind):
+        """Fast-mode SDCA solver: "auto" (default), "chain" or "gram" (cocoa_set_solver)."""
+        C.check(C.lib().cocoa_set_solver(self.h, C.SOLVERS[kind]), self.h)
+
     def init(self, method, n, num_rounds, local_iters, lam, beta=1.0, gamma=1.0, debug_iter=10, seed=0,
              chkpt_iter=100, w_init=None):
         self.params = C.Params(n, num_rounds, local_iters, 0, lam, beta, gamma)

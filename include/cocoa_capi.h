@@ -142,6 +142,18 @@ int cocoa_set_test(cocoa_ctx *ctx, const int64_t *row_ptr, const int32_t *col, c
                    int64_t n_rows);
 
 /* ---- solver ---------------------------------------------------------------*/
+/* Local solver of the SDCA methods in fast mode (strict mode always runs the
+ * chain solver, which sums every dot in the reference's order):
+ *   CHAIN -- each step gathers deltaW (or w) at its row and reduces the dot;
+ *   GRAM  -- the dot is a lagged gather plus Gram corrections of the last 64
+ *            steps, so the sequential chain does no memory access;
+ *   AUTO  -- GRAM on sparse rows (mean nnz/row <= 512), CHAIN on long dense
+ *            rows.  Takes effect at the next cocoa_init. */
+#define COCOA_SOLVER_AUTO 0
+#define COCOA_SOLVER_CHAIN 1
+#define COCOA_SOLVER_GRAM 2
+int cocoa_set_solver(cocoa_ctx *ctx, int kind);
+
 /* Start a run: alpha = 0 (CoCoA.scala:33), w = w_init (NULL = zeros,
  * hingeDriver.scala:75), scaling per method (CoCoA.scala:37). */
 int cocoa_init(cocoa_ctx *ctx, const cocoa_params *params, const cocoa_debug *debug, int method, const double *w_init);
@@ -225,7 +237,8 @@ int cocoa_samples(cocoa_ctx *ctx, int32_t part, int32_t seed_plus_t, int32_t cou
 #define COCOA_K_APPLY 3
 #define COCOA_K_EVAL 4
 #define COCOA_K_PLAN 5   /* per-round step plan (row offsets, x.w) of the SDCA loaders */
-#define COCOA_K_COUNT 6
+#define COCOA_K_GRAM 6   /* Gram rows of the round (Gram-window solver) */
+#define COCOA_K_COUNT 7
 /* enable = 1: bracket every launch with HIP events on the context stream. */
 int cocoa_stats_enable(cocoa_ctx *ctx, int enable);
 /* total device milliseconds and launch count per kernel id since last reset */
