@@ -591,7 +591,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     } else
         HIPCHK(hipMemsetAsync(ctx->w.p, 0, sizeof(double) * (size_t)d, s));
     ctx->alpha.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
-    ctx->alpha_work.alloc(sizeof(double) * (size_t)std::max<int64_t>(n, 1));
+    ctx->alpha_work.alloc(sizeof(double) * (size_t)(std::max<int64_t>(n, 1) + K));  // + a sink per partition
     if (ctx->zstream) HIPCHK(hipStreamSynchronize(ctx->zstream));  // no re-zeroing in flight
     ctx->zpending[0] = ctx->zpending[1] = false;
     ctx->zero_owed = -1;
@@ -662,9 +662,9 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                     (ctx->solver_kind == COCOA_SOLVER_GRAM || (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0));
     if (ctx->use_gram) {
         ctx->status.alloc_zero(sizeof(int) * 4, s);
-        ctx->nbatch = (H + 31) / 32;
+        ctx->nbatch = (H + 15) / 16;  // kGB = 16 steps per batch (solver_gram.h)
         if (method != COCOA_METHOD_MBCD)
-            ctx->gt.alloc(sizeof(double) * (size_t)K * (size_t)ctx->nbatch * 32 * 64);
+            ctx->gt.alloc(sizeof(double) * (size_t)K * (size_t)ctx->nbatch * 16 * 64);
         else
             ctx->gt.free();
     } else {
@@ -796,6 +796,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.dw = dws;
             g.gt = c->gt.p ? c->gt.as<double>() : nullptr;
             g.status = c->status.as<int>();
+            g.prof = c->sa.prof;
             g.d = d;
             g.H = H;
             g.nbatch = c->nbatch;

@@ -129,10 +129,11 @@ struct GramSolverArgs {
     double* dw;               // K_loc * d private deltaW (zero on entry)
     const double* gt;         // Gram rows of the round (gram_kernel)
     int* status;              // set to 1 if a hand-off wait timed out (the launch then drains)
+    uint64_t* prof;           // optional [K][4 waves][4]: wait cycles, total cycles (diagnostics)
     int64_t d;
     int32_t H, nbatch;
     int32_t raw_alpha;
-    int32_t pad;
+    int32_t hot;              // columns [0, hot) of deltaW live in LDS (set by launch_solver_gram)
     double lam_n, inv_lam_n;
     double sigma;             // sigma' = K gamma (CoCoA+)
     double scaling;
@@ -180,7 +181,7 @@ int eval_fast_blocks(int64_t n, int64_t n_test);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 // Gram-window solver: lds bytes for a partition of max_nl rows (alpha in LDS
 // when it fits, else in alpha_work)
-size_t gram_solver_lds(int32_t max_nl, bool* alv_lds);
+size_t gram_solver_lds(int32_t max_nl, int64_t d, bool* alv_lds, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, int32_t max_nl, hipStream_t s);
 

@@ -1,6 +1,7 @@
 // Fast translation unit (-ffp-contract=fast): wave-tree dot products and
 // fused multiply-adds.  Results agree with the strict path within the 1e-9
 // relative tolerance of BASELINE.json's north_star.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.h"
@@ -19,12 +20,17 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
 void launch_plan_fast(const PlanArgs& a, hipStream_t s) { launch_plan_impl<false>(a, s); }
 
 // ------------------------------------------------- Gram-window solver --
-size_t gram_solver_lds(int32_t max_nl, bool* alv_lds) {
+size_t gram_solver_lds(int32_t max_nl, int64_t d, bool* alv_lds, int32_t* hot) {
+    constexpr size_t kLds = 160 * 1024;
     const size_t base = (sizeof(GramSolverLds) + 15) & ~(size_t)15;
-    const size_t al = sizeof(double) * (size_t)(max_nl > 0 ? max_nl : 1);
-    const bool fits = base + al <= 160 * 1024;
+    const size_t al = (sizeof(double) * (size_t)(max_nl + 1) + 15) & ~(size_t)15;  // + the sink of padding steps
+    const bool fits = base + al <= kLds;
+    const size_t used = fits ? base + al : base;
+    // the most frequent columns (device order) of deltaW in the remaining LDS
+    const int64_t h = std::min<int64_t>(d, (int64_t)((kLds - used) / sizeof(double)) & ~(int64_t)63);
     if (alv_lds) *alv_lds = fits;
-    return fits ? base + al : base;
+    if (hot) *hot = (int32_t)std::max<int64_t>(h, 0);
+    return used + sizeof(double) * (size_t)std::max<int64_t>(h, 0);
 }
 
 void launch_gram(const GramArgs& a, hipStream_t s) {
@@ -47,11 +53,12 @@ static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t
 
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, int32_t max_nl, hipStream_t s) {
     bool alv = false;
-    const size_t lds = gram_solver_lds(max_nl, &alv);
+    GramSolverArgs g = a;
+    const size_t lds = gram_solver_lds(max_nl, a.d, &alv, &g.hot);
 #define COCOA_SG(M)                        \
     do {                                   \
-        if (alv) launch_sg<M, true>(a, grid, lds, s);  \
-        else launch_sg<M, false>(a, grid, lds, s);     \
+        if (alv) launch_sg<M, true>(g, grid, lds, s);  \
+        else launch_sg<M, false>(g, grid, lds, s);     \
     } while (0)
     if (mode == MODE_PLUS) COCOA_SG(MODE_PLUS);
     else if (mode == MODE_COCOA) COCOA_SG(MODE_COCOA);

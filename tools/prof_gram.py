@@ -1,0 +1,44 @@
+"""Diagnostics for the Gram-window solver on the C2 shape: per-wave hand-off
+wait cycles vs total cycles (chain, scatter, base, loader) and kernel times."""
+import json
+import sys
+
+import numpy as np
+
+sys.path.insert(0, ".")
+from cocoa_amd import Engine, configs  # noqa: E402
+
+
+def main():
+    method = sys.argv[1] if len(sys.argv) > 1 else "cocoa+"
+    sh = configs.share("c2")
+    e = Engine(strict=False)
+    e.set_train(sh.train, part_begin=sh.part_begin, num_parts_global=sh.k_glob)
+    e.set_solver("gram")
+    e.init(method, sh.n_glob, 100, sh.H, sh.lam)
+    e.solver_profile(True)
+    for t in (1, 2):
+        e.round(t)
+    e.sync()
+    e.stats_reset()
+    e.stats_enable(True)
+    for t in (3, 4, 5):
+        e.round(t)
+    e.sync()
+    st = e.kernel_stats()
+    full = e.solver_profile_read().reshape(e.K_loc, 32).astype(np.float64)
+    raw = full[:, :16].reshape(e.K_loc, 4, 4)
+    mem = full[:, 16:20].mean(axis=0)
+    roles = ["chain", "memory", "loader", "idle"]
+    out = {"method": method, "kernel_ms": {k: v["total_ms"] / max(v["launches"], 1) for k, v in st.items()},
+           "waves": {r: {"wait_cyc_mean": float(raw[:, i, 0].mean()), "total_cyc_mean": float(raw[:, i, 1].mean()),
+                         "wait_frac": float(raw[:, i, 0].sum() / max(raw[:, i, 1].sum(), 1))}
+                     for i, r in enumerate(roles)},
+           "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
+           "memory_phases_cyc_per_batch": dict(zip(["pack_fetch", "atomics", "gathers", "rowsums"],
+                                                   (mem / ((sh.H + 31) // 32)).tolist()))}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
