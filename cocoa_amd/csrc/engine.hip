@@ -805,7 +805,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.inv_lam_n = 1.0 / c->sa.lam_n;
             g.sigma = c->method == COCOA_METHOD_COCOA_PLUS ? c->sa.sigma : 1.0;
             g.scaling = c->scaling;
-            c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(solver_mode(c->method), g, K, c->max_nl, s); });
+            c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(solver_mode(c->method), g, K, s); });
         } else if (is_sdca(c->method)) {
             c->timed(COCOA_K_SOLVER, [&] {
                 if (c->strict)

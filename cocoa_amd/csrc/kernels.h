@@ -125,7 +125,7 @@ struct GramSolverArgs {
     const int32_t* col;
     const double* val;
     double* alpha;            // alphaOld (persistent)
-    double* alpha_work;       // working alpha when it does not fit in LDS
+    double* alpha_work;       // working alpha (n + K: a sink after each partition)
     double* dw;               // K_loc * d private deltaW (zero on entry)
     const double* gt;         // Gram rows of the round (gram_kernel)
     int* status;              // set to 1 if a hand-off wait timed out (the launch then drains)
@@ -134,6 +134,8 @@ struct GramSolverArgs {
     int32_t H, nbatch;
     int32_t raw_alpha;
     int32_t hot;              // columns [0, hot) of deltaW live in LDS (set by launch_solver_gram)
+    int32_t diag;             // diagnostics only (COCOA_GRAM_DIAG): 1 skip scatter atomics, 2 skip gathers
+    int32_t pad2;
     double lam_n, inv_lam_n;
     double sigma;             // sigma' = K gamma (CoCoA+)
     double scaling;
@@ -181,9 +183,9 @@ int eval_fast_blocks(int64_t n, int64_t n_test);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 // Gram-window solver: lds bytes for a partition of max_nl rows (alpha in LDS
 // when it fits, else in alpha_work)
-size_t gram_solver_lds(int32_t max_nl, int64_t d, bool* alv_lds, int32_t* hot);
+size_t gram_solver_lds(int64_t d, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
-void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, int32_t max_nl, hipStream_t s);
+void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s);
 
 // strict translation unit
 void launch_plan_strict(const PlanArgs& a, hipStream_t s);

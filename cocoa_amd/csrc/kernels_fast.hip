@@ -20,17 +20,13 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
 void launch_plan_fast(const PlanArgs& a, hipStream_t s) { launch_plan_impl<false>(a, s); }
 
 // ------------------------------------------------- Gram-window solver --
-size_t gram_solver_lds(int32_t max_nl, int64_t d, bool* alv_lds, int32_t* hot) {
+size_t gram_solver_lds(int64_t d, int32_t* hot) {
     constexpr size_t kLds = 160 * 1024;
     const size_t base = (sizeof(GramSolverLds) + 15) & ~(size_t)15;
-    const size_t al = (sizeof(double) * (size_t)(max_nl + 1) + 15) & ~(size_t)15;  // + the sink of padding steps
-    const bool fits = base + al <= kLds;
-    const size_t used = fits ? base + al : base;
     // the most frequent columns (device order) of deltaW in the remaining LDS
-    const int64_t h = std::min<int64_t>(d, (int64_t)((kLds - used) / sizeof(double)) & ~(int64_t)63);
-    if (alv_lds) *alv_lds = fits;
-    if (hot) *hot = (int32_t)std::max<int64_t>(h, 0);
-    return used + sizeof(double) * (size_t)std::max<int64_t>(h, 0);
+    const int64_t h = std::max<int64_t>(0, std::min<int64_t>(d, (int64_t)((kLds - base) / sizeof(double)) & ~(int64_t)63));
+    if (hot) *hot = (int32_t)h;
+    return base + sizeof(double) * (size_t)h;
 }
 
 void launch_gram(const GramArgs& a, hipStream_t s) {
@@ -44,26 +40,25 @@ void launch_gram(const GramArgs& a, hipStream_t s) {
     if (grid > 0) gram_kernel<<<(unsigned)grid, 256, sizeof(GramLds), s>>>(a);
 }
 
-template <int MODE, bool ALV>
+template <int MODE>
 static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
-    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, ALV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    solver_gram_kernel<MODE, ALV><<<grid, 256, lds, s>>>(a);
+    solver_gram_kernel<MODE><<<grid, kGThreads, lds, s>>>(a);
 }
 
-void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, int32_t max_nl, hipStream_t s) {
-    bool alv = false;
+void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s) {
     GramSolverArgs g = a;
-    const size_t lds = gram_solver_lds(max_nl, a.d, &alv, &g.hot);
-#define COCOA_SG(M)                        \
-    do {                                   \
-        if (alv) launch_sg<M, true>(g, grid, lds, s);  \
-        else launch_sg<M, false>(g, grid, lds, s);     \
-    } while (0)
-    if (mode == MODE_PLUS) COCOA_SG(MODE_PLUS);
-    else if (mode == MODE_COCOA) COCOA_SG(MODE_COCOA);
-    else COCOA_SG(MODE_MBCD);
-#undef COCOA_SG
+    size_t lds = gram_solver_lds(a.d, &g.hot);
+    if (const char* e = getenv("COCOA_GRAM_HOT")) {  // diagnostics: cap the LDS-resident columns
+        const int32_t h = std::min<int32_t>(g.hot, (int32_t)atoi(e) & ~63);
+        lds -= sizeof(double) * (size_t)(g.hot - h);
+        g.hot = h;
+    }
+    if (const char* e = getenv("COCOA_GRAM_DIAG")) g.diag = atoi(e);  // timing experiments: results invalid
+    if (mode == MODE_PLUS) launch_sg<MODE_PLUS>(g, grid, lds, s);
+    else if (mode == MODE_COCOA) launch_sg<MODE_COCOA>(g, grid, lds, s);
+    else launch_sg<MODE_MBCD>(g, grid, lds, s);
 }
 
 // ----------------------------------------------------------- fused eval --

@@ -56,15 +56,19 @@ constexpr int kGSlots = 64;              // window slots = lanes
 constexpr int kGNB = kGSlots / kGB;      // batches in the window
 constexpr int kGRing = 8;                // record / coefficient ring (batches)
 constexpr int kGHot = 64;                // dense hot columns of gram_kernel (device order: most frequent first)
-constexpr int kGMU = 24;                 // 64-entry units per batch the memory wave keeps in registers
-constexpr int kGStage = kGMU * 64;       // staged gather values / products (one batch)
 
 // ----------------------------------------------------------- LDS handoff --
+// The hand-offs order LDS data only (records, coefficients, layouts, staged
+// entries, bases): LDS-only fences, so a release waits for the wave's LDS
+// operations (lgkmcnt) and never for its outstanding global stores / atomics.
 __device__ __forceinline__ int lds_acquire(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    return v;
 }
 __device__ __forceinline__ void lds_release(int* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // Spin (s_sleep) until *p >= v.  Bounded: a wait that outlasts ~2^24 sleeps
 // (far beyond any legitimate hand-off) raises the workgroup's abort flag and
@@ -91,7 +95,10 @@ __device__ __forceinline__ bool wait_ge(const int* p, int v, int* abort_flag, in
 __device__ __forceinline__ double dw_load(const double* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+// gathers of hot columns (deltaW in LDS) load this instead: one line, factor 1
+static __device__ double g_gram_one = 1.0;
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }    // vmcnt(0)
+__device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F); }  // lgkmcnt(0)
 
 // ================================================================ Gram ==
 // Gt[k][j][slot] = x_{s} . x_j for the step s of window slot `slot` in j's
@@ -306,27 +313,48 @@ __global__ __launch_bounds__(256, 1) void gram_kernel(GramArgs a) {
 // with aa = 0 and grad >= 0, or aa = 1 and grad <= 0, the clamp returns aa.
 // An empty row (qii = 0) always gets alpha = 1 (grad = -lambda n < 0):
 // B = 0, E = -1.  MbCD (MinibatchCD.scala:104): A = 0, so B = 0.
+constexpr int kGWin = kGSlots + kGB;     // loader's look-back for alpha forwarding: 5 batches
+constexpr int kGE = 8192;                // staged entries (LDS ring positions)
+constexpr int kGMaxU = 32;               // 64-entry units of a staged batch; larger batches go direct
+constexpr int kGFetch = 2;               // fetch waves
+constexpr int kGThreads = 64 * (3 + kGFetch);
+constexpr int kGGt = 4;                  // Gram-row ring (batches)
+
 struct GRec {                          // one step (64 B)
-    double B, Y, AE, YA;               // AE, YA: set by the chain when the step's slot is filled
+    double B, Y, AE, YA;               // AE, YA: set by the chain (its alpha prefetch or a forward)
     double E;
     int32_t r;                         // sampled row (partition-local); padding steps: the alpha sink
-    int32_t fw;                        // slot of the next step of the window with the same row, -1
-    int32_t pad[4];
+    int32_t fw;                        // ring position (mod 128) of the next step with the same row, -1
+    int32_t fwd;                       // AE / YA already forwarded (the prefetched alpha is stale)
+    int32_t pad[3];
 };
 
+struct GLay {                          // one batch's rows, for the fetch and memory waves
+    int64_t sb[kGB];                   // row starts in the CSR
+    int32_t sx[kGB + 1];               // packed offsets: row i at [sx[i], sx[i+1])
+    int32_t pos;                       // ring position of the staged entries (multiple of 64); -1: direct
+    int32_t nu;                        // 64-entry units
+    int32_t T;                         // entries
+};
+
+// counters (LDS, release / acquire)
+constexpr int kCChain = 0, kCScat = 1, kCBase = 2, kCLoad = 3, kCAbort = 4, kCFreed = 5, kCFetch = 6;
+
 struct GramSolverLds {
-    int cnt[8];                        // 0 chain_done, 1 scat_done, 2 base_done, 3 load_done, 4 abort
+    int cnt[16];
     GRec rec[kGRing * kGB];            // ring: (b % kGRing) * kGB + i
     double coef[kGRing * kGB];         // c_j, same ring (chain -> memory wave)
-    double base[kGSlots];              // base_s per slot
-    int32_t smpwin[kGSlots];           // loader: sampled rows of its window
-    int32_t pdw[kGB];                  // loader: previous occurrence (window position) of its steps
-    double stage[2][kGStage];          // memory wave: staged gather values, then products (by parity)
-    int32_t mx[3][kGB + 1];            // memory wave: packed row offsets (0 scatter, 1 issue, 2 process)
-    int64_t mb[3][kGB];                //   and row starts
-    int32_t mu[3][kGMU];               //   units (row | chunk << 8), first kGMU of each batch
-    int32_t mp[3][kGB + 1];            //   units before row i
+    GLay lay[kGRing];                  // same ring (loader -> fetch / memory waves)
+    double base[kGSlots];              // base_s per slot (memory wave -> chain)
+    double part[kGB][64];              // memory wave: per-lane row partial sums of a batch's products
+    double gring[kGGt][kGB][kGSlots];  // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
+    int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
+    int32_t ecol[kGE];                 // staged entries (fetch waves -> memory wave): column,
+    uint32_t evlo[kGE], evhi[kGE];     //   value (two halves: the LDS DMA moves 4 bytes a lane),
+    uint8_t erow[kGE];                 //   row in the batch (0xFF: past the batch's entries)
 };
+
+static_assert(sizeof(GramSolverLds) <= 160 * 1024, "solver_gram_kernel LDS");
 
 template <int MODE>
 __device__ __forceinline__ void gram_row_consts(const GramSolverArgs& a, double y, double q, double xw, double& B,
@@ -354,110 +382,30 @@ __device__ __forceinline__ int gram_owner(const int32_t* excl, int32_t q) {
     return lo;
 }
 
-// Layout of batch b's rows for the memory wave: packed offsets sx (row i at
-// [sx[i], sx[i+1])), row starts sb, and the 64-entry units (row, chunk) of
-// the first kGMU chunks (lanes of a unit = consecutive entries of one row, so
-// a unit's address is a row start plus the lane).  Returns the entry count;
-// up[i] = units before row i (up[kGB] = all units, may exceed kGMU).
-__device__ __forceinline__ int32_t gram_pack(const GramSolverArgs& a, size_t g0, int32_t b, int32_t* sx, int64_t* sb,
-                                             int32_t* units, int32_t* up) {
-    const int lane = lane_id();
-    const int32_t j = b * kGB + lane;
-    int64_t beg = 0;
-    int32_t z = 0;
-    if (lane < kGB && j < a.H) {
-        beg = a.plan_beg[g0 + j];
-        z = a.plan_z[g0 + j];
-    }
-    const int32_t inc = wave_incl_scan(lane < kGB ? z : 0);
-    const int32_t nc = lane < kGB ? (z + 63) >> 6 : 0;
-    const int32_t uinc = wave_incl_scan(nc);
-    if (lane < kGB) {
-        sx[lane + 1] = inc;
-        sb[lane] = beg;
-        up[lane + 1] = uinc;
-        for (int32_t c = 0, u = uinc - nc; c < nc && u < kGMU; ++c, ++u) units[u] = lane | (c << 8);
-    }
-    if (lane == 0) {
-        sx[0] = 0;
-        up[0] = 0;
-    }
-    wave_lds_sync();
-    return __shfl(inc, kGB - 1, 64);
+// 4 bytes per lane from global memory straight into LDS (lds + 4 * lane)
+__device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
 
-// scatter side: the first min(nunits, NU) units into registers
-template <int NU>
-__device__ __forceinline__ void gram_fetch(const GramSolverArgs& a, const int32_t* sx, const int64_t* sb,
-                                           const int32_t* units, int32_t nunits, int32_t (&cc)[NU],
-                                           double (&vv)[NU]) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        cc[u] = -1;
-        vv[u] = 0.0;
-        if (u < nunits) {
-            const int32_t ut = units[u];
-            const int i = ut & 0xFF;
-            const int32_t e = ((ut >> 8) << 6) + lane;
-            if (e < sx[i + 1] - sx[i]) {
-                cc[u] = a.col[sb[i] + e];
-                vv[u] = a.val[sb[i] + e];
-            }
-        }
-    }
+__device__ __forceinline__ double ring_val(const GramSolverLds& S, int32_t ri) {
+    return __hiloint2double((int)S.evhi[ri], (int)S.evlo[ri]);
 }
 
-// gather side: columns in registers, values straight into the stage buffer
-template <int NU>
-__device__ __forceinline__ void gram_fetch_g(const GramSolverArgs& a, const int32_t* sx, const int64_t* sb,
-                                             const int32_t* units, int32_t nunits, int32_t (&cc)[NU],
-                                             double* stage) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        cc[u] = -1;
-        if (u < nunits) {
-            const int32_t ut = units[u];
-            const int i = ut & 0xFF;
-            const int32_t e = ((ut >> 8) << 6) + lane;
-            if (e < sx[i + 1] - sx[i]) {
-                cc[u] = a.col[sb[i] + e];
-                stage[sx[i] + e] = a.val[sb[i] + e];
-            }
-        }
-    }
-}
-
-// row sums of staged products [0, T) laid out by (sx): lanes < kGB take the
-// rows of <= 64 entries in stored order, the whole wave the longer ones
-__device__ __forceinline__ void gram_row_sums(const int32_t* sx, const double* stage, int32_t T, double* out) {
-    const int lane = lane_id();
-    const int32_t rb = lane < kGB ? sx[lane] : 0, re = lane < kGB ? sx[lane + 1] : 0;
-    double sum = 0.0;
-    if (lane < kGB && re - rb <= 64)
-        for (int32_t q = rb; q < re; ++q) sum += stage[q];
-    uint64_t lm = __ballot(lane < kGB && re - rb > 64);
-    while (lm) {
-        const int i = __builtin_ctzll(lm);
-        lm &= lm - 1;
-        const int32_t b0 = sx[i], b1 = sx[i + 1];
-        double acc = 0.0;
-        for (int32_t q = b0 + lane; q < b1; q += 64) acc += stage[q];
-        const double t = wave_sum(acc);
-        if (lane == i) sum = t;
-    }
-    if (lane < kGB) out[lane] = sum;
-    (void)T;
-}
-
-template <int MODE, bool ALV_LDS>
-__global__ __launch_bounds__(256, 1) void solver_gram_kernel(GramSolverArgs a) {
+// Roles (kGThreads threads, one workgroup per partition):
+//   wave 0       chain  -- the H dependent steps;
+//   wave 1       memory -- per batch b: deltaW += c_j x_j (batch b), then the
+//                          gathers x_s . deltaW of batch b+4, their products
+//                          summed one batch later;
+//   wave 2       loader -- records (update-rule constants, alpha forwarding
+//                          marks) and row layouts, up to kGRing batches ahead;
+//   waves 3..    fetch  -- copy each batch's (column, value) entries into the
+//                          LDS ring (LDS DMA), ahead of the gathers.
+template <int MODE>
+__global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramSolverLds& S = *(GramSolverLds*)lds_raw;
-    // LDS after the hand-off state: deltaW of the hot columns [0, a.hot), then alpha
+    // LDS after the hand-off state: deltaW of the hot columns [0, a.hot)
     double* hotl = (double*)(lds_raw + ((sizeof(GramSolverLds) + 15) & ~(size_t)15));
-    double* alv_l = hotl + a.hot;
     const int32_t hot = a.hot;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int k = blockIdx.x;
@@ -466,306 +414,461 @@ __global__ __launch_bounds__(256, 1) void solver_gram_kernel(GramSolverArgs a) {
     const int32_t nl = (int32_t)(a.part_ptr[k + 1] - p0);
     const size_t g0 = (size_t)k * H;
     double* dwk = a.dw + (size_t)k * a.d;
-    // alpha of the partition, plus a sink at [nl] for the padding steps
-    double* alv = ALV_LDS ? alv_l : a.alpha_work + p0 + k;
+    // working alpha of the partition (global), plus a sink at [nl] for the padding steps
+    double* alv = a.alpha_work + p0 + k;
     const double* gt = a.gt + (size_t)k * a.nbatch * kGB * kGSlots;
+    int* abortf = &S.cnt[kCAbort];
 
-    for (int32_t i = tid; i < nl; i += 256) alv[i] = a.alpha[p0 + i];
-    if (tid == 0) alv[nl] = 0.0;  // sink of the padding steps
-    for (int i = tid; i < kGSlots; i += 256) S.base[i] = 0.0;  // batches 0 .. kGNB-1: deltaW is still zero
-    for (int32_t i = tid; i < hot; i += 256) hotl[i] = 0.0;
-    if (tid < 8) S.cnt[tid] = 0;
+    for (int32_t i = tid; i < nl; i += kGThreads) alv[i] = a.alpha[p0 + i];
+    if (tid == 0) alv[nl] = 0.0;
+    for (int i = tid; i < kGSlots; i += kGThreads) S.base[i] = 0.0;  // batches 0 .. kGNB-1: deltaW is still zero
+    for (int32_t i = tid; i < hot; i += kGThreads) hotl[i] = 0.0;
+    if (tid < 16) S.cnt[tid] = 0;
     __syncthreads();
-    if (tid == 0) S.cnt[2] = kGNB;  // base_done
+    if (tid == 0) S.cnt[kCBase] = kGNB;
     __syncthreads();
-    // diagnostics (a.prof): per wave, cycles spent waiting on hand-offs and in total
     uint64_t wait_cycles = 0;
     uint64_t* pw = a.prof ? &wait_cycles : nullptr;
     const uint64_t t_start = a.prof ? __builtin_readcyclecounter() : 0;
 
     if (wv == 2) {
         // ------------------------------------------------------- loader --
-        for (int32_t b = 0; b < NB; ++b) {
-            // ring slot b % kGRing last held batch b - kGRing
-            if (!wait_ge(&S.cnt[0], b - kGRing + 1, &S.cnt[4], a.status, pw)) break;
-            // window of this batch's steps: batches b-3 .. b (positions 0..63)
-            const int32_t w0 = (b - kGNB + 1) * kGB;
-            const int32_t jw = w0 + lane;
-            S.smpwin[lane] = (jw >= 0 && jw < H) ? a.samples[g0 + jw] : -2;
-            const int32_t j = b * kGB + (lane & (kGB - 1));
-            const bool valid = lane < kGB && j < H;
-            int32_t r = nl;  // padding step: alpha sink
-            double y = 0.0, q = 0.0, xw = 0.0;
-            if (valid) {
-                r = a.samples[g0 + j];
-                y = a.plan_y[g0 + j];
-                q = a.plan_q[g0 + j];
-                xw = a.plan_xw[g0 + j];
+        int32_t cursor = 0;  // ring position of the next staged batch
+        for (int i = lane; i < 2 * kGSlots; i += 64) S.smpwin[i] = -2;
+        // the step's inputs one batch ahead (registers)
+        const int i = lane & (kGB - 1);
+        int32_t xr = nl, xz = 0;
+        double xy = 0.0, xq = 0.0, xxw = 0.0;
+        int64_t xbeg = 0;
+        auto load = [&](int32_t b) {
+            const int32_t j = b * kGB + i;
+            xr = nl;
+            xz = 0;
+            xy = xq = xxw = 0.0;
+            xbeg = 0;
+            if (lane < kGB && j < H) {
+                xr = a.samples[g0 + j];
+                xy = a.plan_y[g0 + j];
+                xq = a.plan_q[g0 + j];
+                xxw = a.plan_xw[g0 + j];
+                xbeg = a.plan_beg[g0 + j];
+                xz = a.plan_z[g0 + j];
             }
-            wave_lds_sync();
-            // previous occurrence of the same row in the window before this step
-            int32_t pd = -1;
-            const int32_t myw = (kGNB - 1) * kGB + (lane & (kGB - 1));
+        };
+        load(0);
+        // batch b's records and layout; the Gram rows of batch b-4 (LDS DMA, their
+        // completion published one iteration later: kCLoad = b+1 means records
+        // <= b and Gram rows <= b-5 are in LDS)
+        const int32_t NL = MODE != MODE_MBCD ? NB + kGGt + 1 : NB;
+        for (int32_t b = 0; b < NL; ++b) {
+            // ring slots (records b % kGRing, Gram rows (b-4) % kGGt) last held batch
+            // b - kGRing: chain and memory wave done with it
+            if (!wait_ge(&S.cnt[kCChain], b - kGRing + 1, abortf, a.status, pw)) break;
+            if (!wait_ge(&S.cnt[kCScat], min(b, NB) - kGRing + 1, abortf, a.status, pw)) break;
+            vm_drain();  // last iteration's loads and DMA
+            if (b < NB) {
+                const int32_t j = b * kGB + i;
+                const bool valid = lane < kGB && j < H;
+                const int32_t r = xr, z = xz;
+                const double y = xy, q = xq, xw = xxw;
+                const int64_t beg = xbeg;
+                if (b + 1 < NB) load(b + 1);
+                const int32_t w0 = b * kGB - kGSlots;  // look-back window: steps [w0, w0 + kGWin)
+                if (lane < kGB) S.smpwin[j & (2 * kGSlots - 1)] = valid ? r : -2;
+                const int32_t inc = wave_incl_scan(lane < kGB ? z : 0);
+                const int32_t T = __shfl(inc, kGB - 1, 64);
+                const int32_t nu = (T + 63) >> 6;
+                wave_lds_sync();
+                // previous occurrence of each step's row in the window before it: lanes =
+                // window positions (0..63: batches b-4 .. b-1; 64 + lane: this batch)
+                int32_t pd = -1;
+                {
+                    const int32_t ra = S.smpwin[(w0 + lane) & (2 * kGSlots - 1)];
+                    const int32_t rb = valid ? r : -3;
+                    const int32_t m = min(kGB, H - b * kGB);
+                    for (int t = 0; t < m; ++t) {
+                        const int32_t rt = __builtin_amdgcn_readlane(r, t);
+                        const uint64_t mb = __ballot(rb == rt && lane < t);
+                        const uint64_t ma = __ballot(ra == rt);
+                        const int32_t p = mb ? kGSlots + 63 - __builtin_clzll(mb) : (ma ? 63 - __builtin_clzll(ma) : -1);
+                        if (lane == t) pd = p;
+                    }
+                }
+                GLay& L = S.lay[b % kGRing];
+                if (lane < kGB) {
+                    GRec& R = S.rec[(b % kGRing) * kGB + lane];
+                    double B = 0.0, E = 0.0, Y = 0.0;
+                    if (valid) gram_row_consts<MODE>(a, y, q, xw, B, E, Y);
+                    R.B = B;
+                    R.E = E;
+                    R.Y = Y;
+                    R.r = r;
+                    R.fw = -1;
+                    R.fwd = 0;
+                    L.sx[lane + 1] = inc;
+                    L.sb[lane] = beg;
+                }
+                if (lane == 0) {
+                    L.sx[0] = 0;
+                    L.T = T;
+                    L.nu = nu;
+                    L.pos = nu <= kGMaxU ? cursor : -1;
+                }
+                if (nu <= kGMaxU) cursor += nu * 64;
+                wave_lds_sync();
+                // mark the earlier occurrence: step w0 + pd forwards its new alpha here
+                if (lane < kGB && pd >= 0) {
+                    const int32_t js = w0 + pd;
+                    S.rec[((js / kGB) % kGRing) * kGB + (js % kGB)].fw = j & (2 * kGSlots - 1);
+                }
+            }
+            const int32_t xg = b - kGGt;  // Gram rows of batch xg: 16 rows x 64 slots
+            if (MODE != MODE_MBCD && xg >= 0 && xg < NB) {
+                const uint32_t* src = (const uint32_t*)(gt + (size_t)xg * kGB * kGSlots);
+                uint32_t* dst = (uint32_t*)&S.gring[xg % kGGt][0][0];
 #pragma unroll 8
-            for (int t = 0; t < kGSlots; ++t) {
-                const int32_t rt = S.smpwin[t];
-                if (valid && t < myw && rt == r) pd = t;
-            }
-            if (lane < kGB) {
-                GRec& R = S.rec[(b % kGRing) * kGB + lane];
-                double B = 0.0, E = 0.0, Y = 0.0;
-                if (valid) gram_row_consts<MODE>(a, y, q, xw, B, E, Y);
-                R.B = B;
-                R.E = E;
-                R.Y = Y;
-                R.r = r;
-                R.fw = -1;
-                S.pdw[lane] = pd;
+                for (int t = 0; t < 2 * kGB * kGSlots / 64; ++t) lds_dma4(src + t * 64 + lane, dst + t * 64);
             }
             wave_lds_sync();
-            // mark the earlier occurrences: step (w0 + pd) forwards its new alpha
-            // to this step's slot (pd < myw, so in batches b-3 .. b)
-            if (lane < kGB && pd >= 0) {
-                const int32_t js = w0 + pd;
-                S.rec[((js / kGB) % kGRing) * kGB + (js % kGB)].fw = j & (kGSlots - 1);
+            if (lane == 0) lds_release(&S.cnt[kCLoad], b + 1);
+        }
+    } else if (wv >= 3) {
+        // -------------------------------------------------------- fetch --
+        const int f = wv - 3;
+        for (int32_t x = f; x < NB; x += kGFetch) {
+            if (!wait_ge(&S.cnt[kCLoad], x + 1, abortf, a.status, pw)) break;
+            const GLay& L = S.lay[x % kGRing];
+            const int32_t pos = L.pos, nu = L.nu, T = L.T;
+            if (pos >= 0 && nu > 0) {
+                // ring space: positions up to pos + 64 nu - kGE released by the memory wave
+                if (!wait_ge(&S.cnt[kCFreed], pos + nu * 64 - kGE, abortf, a.status, pw)) break;
+                for (int32_t u = 0; u < nu; ++u) {
+                    const int32_t q = u * 64 + lane;
+                    const int32_t ri = (pos + u * 64) & (kGE - 1);
+                    const int o = gram_owner(L.sx, q);
+                    if (q < T) {
+                        const int64_t e = L.sb[o] + (q - L.sx[o]);
+                        lds_dma4(a.col + e, S.ecol + ri);
+                        lds_dma4((const uint32_t*)(a.val + e), S.evlo + ri);
+                        lds_dma4((const uint32_t*)(a.val + e) + 1, S.evhi + ri);
+                    }
+                    S.erow[ri + lane] = q < T ? (uint8_t)o : (uint8_t)0xFF;
+                }
+                vm_drain();  // the DMA writes are in LDS
             }
             wave_lds_sync();
-            if (lane == 0) lds_release(&S.cnt[3], b + 1);
+            if (lane == 0) lds_release(&S.cnt[kCFetch + f], x + 1);
         }
     } else if (wv == 1) {
         // ------------------------------------------------------- memory --
-        // layout slots: 0 = scatter batch, 1 = prefetched gather batch,
-        // 2 = gather batch in flight (its products are formed next time)
-        constexpr int NU = kGMU;
-        int32_t cs[NU], cg[NU];
-        double vs[NU], dw[NU];
-        int32_t Ti = 0, Tp = 0;           // entries of the prefetched / in-flight gather batches
-        bool piped = false;               // the in-flight gathers went out (else: gathered synchronously)
         const bool bases = MODE != MODE_MBCD;
-        // deltaW: hot columns in LDS (no same-line L2 atomics), the rest in the slice
+        double hv[kGMaxU], dw[kGMaxU];  // in-flight gathers: staged value (x hot deltaW), loaded deltaW (or 1)
+        uint32_t hrow[(kGMaxU + 5) / 6];  //   and their rows (5 bits per unit, 31 = no entry)
+        int32_t xin = -1;               // batch whose gathers are in flight
         auto dw_add = [&](int32_t c, double v) {
             if (c < hot) __hip_atomic_fetch_add(hotl + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             else unsafeAtomicAdd(dwk + c, v);
         };
         auto dw_get = [&](int32_t c) { return c < hot ? hotl[c] : dw_load(dwk + c); };
-        auto copy_layout = [&](int from, int to) {
-            for (int i = lane; i <= kGB; i += 64) {
-                S.mx[to][i] = S.mx[from][i];
-                S.mp[to][i] = S.mp[from][i];
-                if (i < kGB) S.mb[to][i] = S.mb[from][i];
-            }
-            for (int i = lane; i < NU; i += 64) S.mu[to][i] = S.mu[from][i];
-            wave_lds_sync();
+        auto fetched = [&](int32_t x) {
+            return wait_ge(&S.cnt[kCFetch + x % kGFetch], x + 1, abortf, a.status, pw);
         };
-        // prologue: data of step 0 (gather values of batch kGNB staged by parity)
-        (void)gram_pack(a, g0, 0, S.mx[0], S.mb[0], S.mu[0], S.mp[0]);
-        gram_fetch<NU>(a, S.mx[0], S.mb[0], S.mu[0], S.mp[0][kGB], cs, vs);
-        if (bases && kGNB < NB) {
-            Ti = gram_pack(a, g0, kGNB, S.mx[1], S.mb[1], S.mu[1], S.mp[1]);
-            if (S.mp[1][kGB] <= NU) gram_fetch_g<NU>(a, S.mx[1], S.mb[1], S.mu[1], S.mp[1][kGB], cg, S.stage[kGNB & 1]);
-        }
-        for (int32_t b = 0; b < NB; ++b) {
-            if (!wait_ge(&S.cnt[0], b + 1, &S.cnt[4], a.status, pw)) break;  // the chain finished batch b
-            // 1. the gathers in flight (batch b-1+kGNB): products, row sums
-            const int32_t bp = b - 1 + kGNB;
-            if (bases && b >= 1 && bp < NB) {
-                double* st = S.stage[bp & 1];
-                if (piped) {
-                    const int32_t nu = S.mp[2][kGB];
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        // cg already holds the next prefetch: validity from the layout
-                        if (u < nu) {
-                            const int32_t ut = S.mu[2][u];
-                            const int i = ut & 0xFF;
-                            const int32_t e = ((ut >> 8) << 6) + lane;
-                            if (e < S.mx[2][i + 1] - S.mx[2][i]) {
-                                const int32_t qq = S.mx[2][i] + e;
-                                st[qq] = st[qq] * dw[u];
-                            }
-                        }
-                    }
-                    wave_lds_sync();
-                    gram_row_sums(S.mx[2], st, Tp, S.base + (bp % kGNB) * kGB);
-                } else {
-                    // a batch longer than the registers: gathered and summed here, in passes
-                    double sum = 0.0;
-                    for (int32_t qa = 0; qa < Tp; qa += kGStage) {
-                        const int32_t qb = min(Tp, qa + kGStage);
-                        for (int32_t q0 = qa; q0 < qb; q0 += 64) {
-                            const int32_t qq = q0 + lane;
-                            if (qq < qb) {
-                                const int o = gram_owner(S.mx[2], qq);
-                                const int64_t e = S.mb[2][o] + (qq - S.mx[2][o]);
-                                st[qq - qa] = a.val[e] * dw_get(a.col[e]);
-                            }
-                        }
-                        wave_lds_sync();
-                        if (lane < kGB) {
-                            const int32_t rb = max(S.mx[2][lane], qa), re = min(S.mx[2][lane + 1], qb);
-                            for (int32_t q = rb; q < re; ++q) sum += st[q - qa];
-                        }
-                        wave_lds_sync();
-                    }
-                    if (lane < kGB) S.base[(bp % kGNB) * kGB + lane] = sum;
-                }
-                wave_lds_sync();
-                if (lane == 0) lds_release(&S.cnt[2], bp + 1);
+        uint64_t ph[4] = {0, 0, 0, 0};
+        uint64_t tph = 0;
+        auto stamp = [&](int i) {
+            if (a.prof) {
+                const uint64_t t = __builtin_readcyclecounter();
+                ph[i] += t - tph;
+                tph = t;
             }
+        };
+        for (int32_t b = 0; b < NB; ++b) {
+            if (!wait_ge(&S.cnt[kCChain], b + 1, abortf, a.status, pw)) break;  // the chain finished batch b
+            if (a.prof) tph = __builtin_readcyclecounter();
+            // every load of the previous iteration has landed (step 1 needs the gathers
+            // anyway): the compiler then knows no register is still being written and
+            // issues step 3's loads back to back instead of waiting before each one
+            vm_drain();
+            // 1. products of the gathers in flight -> base of batch xin.  Each lane
+            //    runs over its positions (rows ascend with the unit) and parks one
+            //    partial sum per (row, lane); 4 lanes per row add them up.
+            if (xin >= 0) {
+#pragma unroll
+                for (int i = 0; i < kGB; ++i) S.part[i][lane] = 0.0;
+                int cur = -1;
+                double run = 0.0;
+#pragma unroll
+                for (int u = 0; u < kGMaxU; ++u) {
+                    const int row = (int)((hrow[u / 6] >> (5 * (u % 6))) & 31u);  // 31: no entry
+                    if (row != cur) {
+                        if (cur >= 0 && cur < kGB) S.part[cur][lane] = run;
+                        cur = row;
+                        run = 0.0;
+                    }
+                    run = fma(hv[u], dw[u], run);
+                }
+                if (cur >= 0 && cur < kGB) S.part[cur][lane] = run;
+                wave_lds_sync();
+                const int rr = lane >> 2, qq = (lane & 3) * 16;
+                double s4 = 0.0;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) s4 += S.part[rr][qq + t];
+                s4 += dpp_row_d<0xB1>(s4);  // quad_perm [1,0,3,2]
+                s4 += dpp_row_d<0x4E>(s4);  // quad_perm [2,3,0,1]
+                if ((lane & 3) == 0) S.base[(xin % kGNB) * kGB + rr] = s4;
+                wave_lds_sync();
+                if (lane == 0) lds_release(&S.cnt[kCBase], xin + 1);
+                xin = -1;
+            }
+            stamp(0);
             // 2. deltaW += c_j x_j for the steps of batch b (CoCoA.scala:181-185)
             {
+                const GLay& L = S.lay[b % kGRing];
                 const double* cf = S.coef + (b % kGRing) * kGB;
-                const int32_t nus = S.mp[0][kGB];
-                // the batch's entries are in registers before the first atomic: without
-                // this the compiler waits for every outstanding access (the previous
-                // atomic included) before each one -- an L2 round trip per unit
-                vm_drain();
+                const int32_t pos = L.pos, nu = L.nu;
+                if (pos >= 0) {
+                    if (!fetched(b)) break;
+                    // groups of 4 units: the LDS reads of a group go out together (reading
+                    // past the batch is harmless: those lanes get row 0xFF)
+                    // (every read of a group before its first atomic: an LDS atomic may
+                    // alias them in the compiler's view and would serialise the group)
+                    for (int32_t u0 = 0; u0 < nu; u0 += 8) {
+                        int rw[8];
+                        int32_t cl[8];
+                        double vl[8], cc[8];
 #pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    if (u < nus && cs[u] >= 0) {
-                        const double c = cf[S.mu[0][u] & 0xFF];
-                        if (c != 0.0) dw_add(cs[u], vs[u] * c);
+                        for (int t = 0; t < 8; ++t) {
+                            const int32_t ri = ((pos + (u0 + t) * 64) & (kGE - 1)) + lane;
+                            rw[t] = u0 + t < nu ? S.erow[ri] : 0xFF;
+                            cl[t] = S.ecol[ri];
+                            vl[t] = ring_val(S, ri);
+                        }
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) cc[t] = rw[t] < kGB ? cf[rw[t] & (kGB - 1)] : 0.0;
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < 8; ++t)
+                            if (cc[t] != 0.0 && !(a.diag & 1)) dw_add(cl[t], vl[t] * cc[t]);
+                    }
+                } else {
+                    // a batch too long to stage: straight from the CSR, row by row
+                    for (int i = 0; i < kGB; ++i) {
+                        const double c = cf[i];
+                        if (c == 0.0) continue;
+                        const int32_t z = L.sx[i + 1] - L.sx[i];
+                        const int64_t rb = L.sb[i];
+                        for (int32_t e = lane; e < z; e += 64) dw_add(a.col[rb + e], a.val[rb + e] * c);
                     }
                 }
-                // units past the registers (long rows): row by row
-                for (int i = 0; nus > NU && i < kGB; ++i) {
-                    const int32_t u0 = S.mp[0][i], u1 = S.mp[0][i + 1];
-                    if (u1 <= NU) continue;
-                    const double c = cf[i];
-                    if (c == 0.0) continue;
-                    const int32_t z = S.mx[0][i + 1] - S.mx[0][i];
-                    const int64_t rb = S.mb[0][i];
-                    for (int32_t e = 64 * (u0 < NU ? NU - u0 : 0) + lane; e < z; e += 64)
-                        dw_add(a.col[rb + e], a.val[rb + e] * c);
+                wave_lds_sync();
+                if (lane == 0) {
+                    lds_release(&S.cnt[kCScat], b + 1);  // coefficient / record / layout slot consumed
+                    if (pos >= 0) lds_release(&S.cnt[kCFreed], pos + nu * 64);
                 }
             }
-            wave_lds_sync();
-            if (lane == 0) lds_release(&S.cnt[1], b + 1);  // coefficient ring slot consumed
-            // 3. issue the gathers of batch b+kGNB (they see batch b's atomics and
-            //    nothing later: the next atomics go out after them)
-            Tp = 0;
-            if (bases && b + kGNB < NB) {
-                copy_layout(1, 2);
-                Tp = Ti;
-                piped = S.mp[2][kGB] <= NU;
-                if (piped) {
+            stamp(1);
+            // 3. gathers of batch x = b + kGNB: they see batch b's updates (issued
+            //    above, same wave, same addresses) and nothing later (the next
+            //    atomics go out after step 1 has consumed these loads)
+            const int32_t x = b + kGNB;
+            if (bases && x < NB) {
+                const GLay& L = S.lay[x % kGRing];
+                const int32_t pos = L.pos, nu = L.nu;
+                if (pos >= 0) {
+                    if (!fetched(x)) break;
 #pragma unroll
-                    for (int u = 0; u < NU; ++u) dw[u] = cg[u] >= 0 ? dw_get(cg[u]) : 0.0;
+                    for (int w = 0; w < (kGMaxU + 5) / 6; ++w) hrow[w] = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int u = 0; u < kGMaxU; ++u) {
+                        hv[u] = 0.0;
+                        dw[u] = 1.0;
+                    }
+#pragma unroll
+                    for (int u0 = 0; u0 < kGMaxU; u0 += 8) {
+                        if (u0 < nu) {
+                            int rw[8];
+                            int32_t cl[8];
+                            double vl[8];
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                const int32_t ri = ((pos + (u0 + t) * 64) & (kGE - 1)) + lane;
+                                rw[t] = u0 + t < nu ? S.erow[ri] : 0xFF;
+                                cl[t] = S.ecol[ri];
+                                vl[t] = ring_val(S, ri);
+                            }
+                            double hx[8];
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                const int u = u0 + t;
+                                const int32_t c = rw[t] < kGB ? cl[t] : -1;
+                                // a hot (LDS) or empty lane loads the constant 1 -- one register
+                                // never mixes a global load with an LDS read (that would serialise)
+                                if (!(a.diag & 2)) dw[u] = dw_load(c >= hot ? dwk + c : &g_gram_one);
+                                hx[t] = hotl[(c >= 0 && c < hot) ? c : 0];
+                            }
+                            __builtin_amdgcn_sched_barrier(0);  // all reads of the group out before the products
+#pragma unroll
+                            for (int t = 0; t < 8; ++t) {
+                                const int u = u0 + t;
+                                const bool ok = rw[t] < kGB;
+                                hv[u] = ok ? ((cl[t] < hot) ? vl[t] * hx[t] : vl[t]) : 0.0;
+                                hrow[u / 6] = (hrow[u / 6] & ~(31u << (5 * (u % 6)))) | ((uint32_t)(ok ? rw[t] : 31) << (5 * (u % 6)));
+                            }
+                        }
+                    }
+                    xin = x;
+                } else {
+                    // too long to stage: gathered and summed here
+                    double* bs = S.base + (x % kGNB) * kGB;
+                    for (int i = 0; i < kGB; ++i) {
+                        const int32_t z = L.sx[i + 1] - L.sx[i];
+                        const int64_t rb = L.sb[i];
+                        double acc = 0.0;
+                        for (int32_t e = lane; e < z; e += 64) acc = fma(a.val[rb + e], dw_get(a.col[rb + e]), acc);
+                        const double t = wave_sum(acc);
+                        if (lane == 0) bs[i] = t;
+                    }
+                    wave_lds_sync();
+                    if (lane == 0) lds_release(&S.cnt[kCBase], x + 1);
                 }
             }
-            // 4. prefetch the data of step b+1
-            if (b + 1 < NB) {
-                (void)gram_pack(a, g0, b + 1, S.mx[0], S.mb[0], S.mu[0], S.mp[0]);
-                gram_fetch<NU>(a, S.mx[0], S.mb[0], S.mu[0], S.mp[0][kGB], cs, vs);
-                const int32_t bn = b + 1 + kGNB;
-                if (bases && bn < NB) {
-                    Ti = gram_pack(a, g0, bn, S.mx[1], S.mb[1], S.mu[1], S.mp[1]);
-                    if (S.mp[1][kGB] <= NU) gram_fetch_g<NU>(a, S.mx[1], S.mb[1], S.mu[1], S.mp[1][kGB], cg, S.stage[bn & 1]);
-                }
-            }
+            stamp(2);
         }
         vm_drain();  // the last atomics land before the kernel ends
+        if (a.prof && lane == 0)
+            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * 32 + 16 + i] = ph[i];
     } else if (wv == 0) {
         // -------------------------------------------------------- chain --
         // lane = window slot (step mod 64): sdot = base + Gram corrections
-        bool ok = wait_ge(&S.cnt[3], min(kGNB, NB), &S.cnt[4], a.status, pw);
+        const int32_t ahead = MODE != MODE_MBCD ? kGGt + 2 : 0;  // kCLoad needed for batch g: g + 1 + kGNB (records), g + 6 (Gram rows)
+        bool ok = wait_ge(&S.cnt[kCLoad], MODE != MODE_MBCD ? ahead : min(kGNB + 1, NB), abortf, a.status, pw);
         double acc = 0.0;
-        // fill: this lane's slot takes the step (lane & 15) of batch b
-        auto fill = [&](int32_t b) {
-            GRec& R = S.rec[(b % kGRing) * kGB + (lane & (kGB - 1))];
+        if (ok && lane / kGB < NB) {
+            GRec& R = S.rec[(lane / kGB) * kGB + (lane & (kGB - 1))];
             const double aa = alv[R.r];
             R.AE = aa - R.E;
             R.YA = R.Y * aa;
-            acc = 0.0;
-        };
-        if (ok && lane / kGB < NB) fill(lane / kGB);
-        wave_lds_sync();
-        double gcur[kGB], gnxt[kGB];
-#pragma unroll
-        for (int i = 0; i < kGB; ++i) {
-            gnxt[i] = 0.0;
-            gcur[i] = (MODE != MODE_MBCD && i < H) ? __builtin_nontemporal_load(gt + (size_t)i * kGSlots + lane) : 0.0;
         }
-        for (int32_t g = 0; ok && g < NB; ++g) {
+        wave_lds_sync();
+        // One batch.  Alpha of batch g+4 is loaded at the start of batch g (rows met
+        // again in batches g .. g+4 are forwarded instead) and written into its
+        // records at the end of batch g+1, a batch after the load: `aissue` / `afill`
+        // alternate between two registers (no copy of a register still being loaded).
+        auto batch = [&](int32_t g, double& aissue, const double& afill) -> bool {
             const int q4 = g % kGNB;          // this batch's quarter of the lanes
             const bool mine = lane / kGB == q4;
-            if (MODE != MODE_MBCD && !wait_ge(&S.cnt[2], g + 1, &S.cnt[4], a.status, pw)) break;
-            // coefficient ring slot g % kGRing held batch g - kGRing: consumed?
-            if (!wait_ge(&S.cnt[1], g - kGRing + 1, &S.cnt[4], a.status, pw)) break;
-            if (mine) acc += S.base[lane];
-            const int32_t m = min(kGB, H - g * kGB);
-            // next batch's Gram rows into registers while this one runs
             if (MODE != MODE_MBCD) {
-#pragma unroll
-                for (int i = 0; i < kGB; ++i) {
-                    const int32_t jn = (g + 1) * kGB + i;
-                    gnxt[i] = jn < H ? __builtin_nontemporal_load(gt + (size_t)jn * kGSlots + lane) : 0.0;
-                }
+                if (!wait_ge(&S.cnt[kCBase], g + 1, abortf, a.status, pw)) return false;
+                if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw)) return false;
+            } else if (!wait_ge(&S.cnt[kCLoad], min(g + kGNB + 1, NB), abortf, a.status, pw)) {
+                return false;
             }
-            GRec* rg = S.rec + (g % kGRing) * kGB;
+            // coefficient ring slot g % kGRing held batch g - kGRing: consumed?
+            if (!wait_ge(&S.cnt[kCScat], g - kGRing + 1, abortf, a.status, pw)) return false;
+            {
+                const int32_t g4 = g + kGNB;
+                const GRec& R4 = S.rec[(g4 % kGRing) * kGB + (lane & (kGB - 1))];
+                aissue = alv[(mine && g4 < NB) ? R4.r : nl];  // one load for every lane (the sink otherwise)
+            }
+            if (mine) acc += S.base[lane];
+            double gcur[kGB];
+#pragma unroll
+            for (int i = 0; i < kGB; ++i) gcur[i] = MODE != MODE_MBCD ? S.gring[g % kGGt][i][lane] : 0.0;
             double* cfo = S.coef + (g % kGRing) * kGB;
             const int slot0 = q4 * kGB;
-            // records one step ahead (uniform LDS reads)
-            double nB = rg[0].B, nY = rg[0].Y, nAE = rg[0].AE, nYA = rg[0].YA, nE = rg[0].E;
-            int32_t nR = rg[0].r, nF = rg[0].fw;
+            // this batch's records in the lanes of its quarter (lane slot0 + i holds step
+            // i, next to its accumulator): every step evaluates the update rule on all
+            // lanes at once and broadcasts one coefficient
+            double rB = 0.0, rY = 0.0, rAE = 0.0, rYA = 0.0, rE = 0.0;
+            int32_t rR = nl, rF = -1;
+            if (mine) {
+                const GRec& R = S.rec[(g % kGRing) * kGB + (lane & (kGB - 1))];
+                rB = R.B;
+                rY = R.Y;
+                rAE = R.AE;
+                rYA = R.YA;
+                rE = R.E;
+                rR = R.r;
+                rF = R.fw;
+            }
+            lgkm_drain();  // records and Gram rows in: no LDS wait inside the steps
+            const uint32_t fwm = (uint32_t)(__ballot(mine && rF >= 0) >> slot0) & 0xFFFFu;  // steps that forward
+            // 16 steps, padding steps included (their record is inert: B = Y = YA = 0,
+            // row = the sink).  Step i: nt = clamp(AE - B sdot) with sdot = acc on its
+            // lane; c = Y nt - YA; acc += c G(., j).  Lanes of steps <= i have G = 0, so
+            // a step's lane keeps its final sdot and the batch's nt / c are recomputed
+            // once at the end for the alpha and coefficient stores.
 #pragma unroll
             for (int i = 0; i < kGB; ++i) {
-                if (i < m) {
-                    const double sB = nB, sY = nY, sAE = nAE, sYA = nYA;
-                    const int32_t sr = nR, sf = uni(nF);
-                    const int in = i + 1 < m ? i + 1 : i;
-                    nB = rg[in].B;
-                    nY = rg[in].Y;
-                    nAE = rg[in].AE;
-                    nYA = rg[in].YA;
-                    nE = rg[in].E;
-                    nR = rg[in].r;
-                    nF = rg[in].fw;
-                    const double sdot = readlane_d(acc, slot0 + i);
-                    // CoCoA.scala:159-186 / MinibatchCD.scala:104-123 (see above)
-                    const double nt = fmin(fmax(fma(-sB, sdot, sAE), 0.0), 1.0);
-                    const double cf = fma(sY, nt, -sYA);
-                    if (MODE != MODE_MBCD) acc = fma(cf, gcur[i], acc);
-                    alv[sr] = nt;          // every lane: same address, same value
-                    cfo[i] = cf;
-                    if (sf >= 0) {
-                        // a later step of the window samples the same row: its aa is nt
-                        const int32_t sp = g * kGB + ((sf - g * kGB) & (kGSlots - 1));
+                // CoCoA.scala:159-186 / MinibatchCD.scala:104-123 (see above)
+                const double nt = fmin(fmax(fma(-rB, acc, rAE), 0.0), 1.0);
+                if (MODE != MODE_MBCD) {
+                    const double cf = readlane_d(fma(rY, nt, -rYA), slot0 + i);
+                    acc = fma(cf, gcur[i], acc);
+                }
+                if (fwm & (1u << i)) {
+                    // a later step (<= 79 steps on) samples the same row: its aa is nt
+                    const double nts = readlane_d(nt, slot0 + i);
+                    const int32_t sf = __builtin_amdgcn_readlane(rF, slot0 + i);
+                    const int32_t sp = g * kGB + ((sf - g * kGB) & (2 * kGSlots - 1));
+                    if (sp < (g + 1) * kGB) {
+                        if (lane == slot0 + (sp - g * kGB)) {  // this batch: its lane's registers
+                            rAE = nts - rE;
+                            rYA = rY * nts;
+                        }
+                        if (lane == slot0 + i) rR = nl;  // the later step stores the row's alpha
+                    } else {
                         GRec& T = S.rec[((sp / kGB) % kGRing) * kGB + (sp % kGB)];
                         const double tE = T.E, tY = T.Y;
-                        T.AE = nt - tE;
-                        T.YA = tY * nt;
-                        if (sp == g * kGB + i + 1) {
-                            nAE = nt - nE;
-                            nYA = nY * nt;
-                        }
+                        T.AE = nts - tE;
+                        T.YA = tY * nts;
+                        T.fwd = 1;
                     }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < kGB; ++i) gcur[i] = gnxt[i];
-            wave_lds_sync();
-            if (lane == 0) lds_release(&S.cnt[0], g + 1);
-            // refill this quarter with batch g + kGNB
-            if (g + kGNB < NB) {
-                if (!wait_ge(&S.cnt[3], g + kGNB + 1, &S.cnt[4], a.status, pw)) break;
-                if (mine) fill(g + kGNB);
-                wave_lds_sync();
+            {
+                const double nt = fmin(fmax(fma(-rB, acc, rAE), 0.0), 1.0);
+                const double cf = fma(rY, nt, -rYA);
+                if (mine) {
+                    alv[rR] = nt;
+                    cfo[lane & (kGB - 1)] = cf;
+                }
             }
+            wave_lds_sync();
+            if (lane == 0) lds_release(&S.cnt[kCChain], g + 1);
+            // this quarter now accumulates for batch g+4
+            if (mine) acc = 0.0;
+            // alpha of batch g+3 (loaded at the start of batch g-1 by the previous
+            // quarter), unless a forward already set it
+            const int32_t g3 = g + kGNB - 1;
+            if (g >= 1 && g3 < NB && lane / kGB == (g + kGNB - 1) % kGNB) {
+                GRec& R3 = S.rec[(g3 % kGRing) * kGB + (lane & (kGB - 1))];
+                if (!R3.fwd) {
+                    R3.AE = afill - R3.E;
+                    R3.YA = R3.Y * afill;
+                }
+            }
+            wave_lds_sync();
+            return true;
+        };
+        double aA = 0.0, aB = 0.0;
+        for (int32_t g = 0; ok && g < NB; g += 2) {
+            if (!batch(g, aA, aB)) break;
+            if (g + 1 < NB && !batch(g + 1, aB, aA)) break;
         }
     }
-    if (a.prof && lane == 0) {
-        uint64_t* pr = a.prof + ((size_t)k * 4 + wv) * 4;
+    if (a.prof && lane == 0 && wv < 4) {
+        uint64_t* pr = a.prof + (size_t)k * 32 + wv * 4;  // [k][32]: waves 0..3 at 0..15, memory phases at 16..19
         pr[0] = wait_cycles;
         pr[1] = __builtin_readcyclecounter() - t_start;
     }
     __syncthreads();
-    for (int32_t i = tid; i < hot; i += 256) dwk[i] = hotl[i];  // the slice is zero there: plain stores
+    for (int32_t i = tid; i < hot; i += kGThreads) dwk[i] = hotl[i];  // the slice is zero there: plain stores
     // alpha = alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101, MinibatchCD.scala:127-128)
     if (a.raw_alpha) {
-        for (int32_t i = tid; i < nl; i += 256) a.alpha[p0 + i] = alv[i];
+        for (int32_t i = tid; i < nl; i += kGThreads) a.alpha[p0 + i] = alv[i];
     } else {
-        for (int32_t i = tid; i < nl; i += 256) {
+        for (int32_t i = tid; i < nl; i += kGThreads) {
             const double old = a.alpha[p0 + i];
             a.alpha[p0 + i] = old + ((alv[i] - old) * a.scaling);
         }

@@ -29,14 +29,14 @@ def main():
     full = e.solver_profile_read().reshape(e.K_loc, 32).astype(np.float64)
     raw = full[:, :16].reshape(e.K_loc, 4, 4)
     mem = full[:, 16:20].mean(axis=0)
-    roles = ["chain", "memory", "loader", "idle"]
+    roles = ["chain", "memory", "loader", "fetch0"]
     out = {"method": method, "kernel_ms": {k: v["total_ms"] / max(v["launches"], 1) for k, v in st.items()},
            "waves": {r: {"wait_cyc_mean": float(raw[:, i, 0].mean()), "total_cyc_mean": float(raw[:, i, 1].mean()),
                          "wait_frac": float(raw[:, i, 0].sum() / max(raw[:, i, 1].sum(), 1))}
                      for i, r in enumerate(roles)},
            "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
-           "memory_phases_cyc_per_batch": dict(zip(["pack_fetch", "atomics", "gathers", "rowsums"],
-                                                   (mem / ((sh.H + 31) // 32)).tolist()))}
+           "memory_phases_cyc_per_batch": dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
+                                                   (mem / ((sh.H + 15) // 16)).tolist()))}
     print(json.dumps(out))
 
 
