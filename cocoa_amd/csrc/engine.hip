@@ -158,6 +158,17 @@ struct cocoa_ctx {
     bool use_gram = false;
     DevBuf gt, status;  // status: set by a Gram-solver launch whose hand-off timed out
     int32_t nbatch = 0;
+    // Round t+1's samples and Gram rows are computed on gstream while round t's
+    // solver runs (the sample sequence depends on seed + t only, the Gram rows
+    // on the samples and the data): two (samples, gt) buffers, b and 1-b.
+    DevBuf samples2, gt2;
+    hipStream_t gstream = nullptr;
+    hipEvent_t g_ready = nullptr, s_done[2] = {nullptr, nullptr};
+    int32_t pre_t = -1, pre_buf = 0;  // round prefetched into buffer pre_buf (-1: none)
+    void gram_quiesce() {  // no prefetch in flight, none pending
+        if (gstream) HIPCHK(hipStreamSynchronize(gstream));
+        pre_t = -1;
+    }
     DevBuf plan_beg, plan_z, plan_y, plan_q, plan_xw;
     // x.w of every train row for the current w, written by the fast eval pass
     // (eval v4) and reused by the next round's plan; false once w moves
@@ -188,16 +199,20 @@ struct cocoa_ctx {
     }
     template <class F>
     void timed(int kid, F&& f) {
+        timed_on(stream, kid, f);
+    }
+    template <class F>
+    void timed_on(hipStream_t st, int kid, F&& f) {
         if (!stats) {
             f();
             HIPCHK(hipGetLastError());
             return;
         }
         hipEvent_t a = get_ev(), b = get_ev();
-        HIPCHK(hipEventRecord(a, stream));
+        HIPCHK(hipEventRecord(a, st));
         f();
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(b, stream));
+        HIPCHK(hipEventRecord(b, st));
         pending.push_back({kid, a, b});
         if (pending.size() > 4096) drain();
     }
@@ -215,6 +230,12 @@ struct cocoa_ctx {
     }
     ~cocoa_ctx() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (gstream) {
+            (void)hipStreamSynchronize(gstream);
+            (void)hipStreamDestroy(gstream);
+            (void)hipEventDestroy(g_ready);
+            for (auto e : s_done) (void)hipEventDestroy(e);
+        }
         delete comm;
         if (zstream) {
             (void)hipStreamSynchronize(zstream);
@@ -377,6 +398,7 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
                                const int32_t* col, const double* val, const double* y, int64_t n_rows,
                                int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
     CAPI_BEGIN(ctx)
+    ctx->gram_quiesce();  // a Gram prefetch reads the CSR being replaced
     require(num_parts >= 1 && part_ptr && row_ptr && y && n_rows >= 0 && num_features >= 1, COCOA_E_ARG,
             "cocoa_set_train: bad argument");
     require(part_begin >= 0 && num_parts_global >= part_begin + num_parts, COCOA_E_ARG,
@@ -593,6 +615,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     ctx->alpha.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
     ctx->alpha_work.alloc(sizeof(double) * (size_t)(std::max<int64_t>(n, 1) + K));  // + a sink per partition
     if (ctx->zstream) HIPCHK(hipStreamSynchronize(ctx->zstream));  // no re-zeroing in flight
+    ctx->gram_quiesce();                                            // no Gram prefetch in flight
     ctx->zpending[0] = ctx->zpending[1] = false;
     ctx->zero_owed = -1;
     ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * d), s);
@@ -663,12 +686,33 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     if (ctx->use_gram) {
         ctx->status.alloc_zero(sizeof(int) * 4, s);
         ctx->nbatch = (H + 15) / 16;  // kGB = 16 steps per batch (solver_gram.h)
-        if (method != COCOA_METHOD_MBCD)
-            ctx->gt.alloc(sizeof(double) * (size_t)K * (size_t)ctx->nbatch * 16 * 64);
-        else
+        if (method != COCOA_METHOD_MBCD) {
+            const size_t gtb = sizeof(double) * (size_t)K * (size_t)ctx->nbatch * 16 * 64;
+            ctx->gt.alloc(gtb);
+            // the next round's (samples, Gram rows) beside this round's, when they fit
+            size_t free_b = 0, total_b = 0;
+            HIPCHK(hipMemGetInfo(&free_b, &total_b));
+            if (free_b > gtb + sizeof(int32_t) * (size_t)ctx->samples_cap + ((size_t)1 << 30)) {
+                ctx->gt2.alloc(gtb);
+                ctx->samples2.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
+                if (!ctx->gstream) {
+                    HIPCHK(hipStreamCreateWithFlags(&ctx->gstream, hipStreamNonBlocking));
+                    HIPCHK(hipEventCreateWithFlags(&ctx->g_ready, hipEventDisableTiming));
+                    for (auto& e : ctx->s_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                }
+            } else {
+                ctx->gt2.free();
+                ctx->samples2.free();
+            }
+        } else {
             ctx->gt.free();
+            ctx->gt2.free();
+            ctx->samples2.free();
+        }
     } else {
         ctx->gt.free();
+        ctx->gt2.free();
+        ctx->samples2.free();
     }
     a.plan_beg = nullptr;
     a.plan_z = nullptr;
@@ -707,6 +751,21 @@ static bool dw_double_buffer(size_t bytes) {
     return bytes >= ((size_t)1 << 30);
 }
 
+static GramArgs gram_args(cocoa_ctx* c, const int32_t* samples, double* gt) {
+    GramArgs ga{};
+    ga.part_ptr = c->part_ptr.as<int64_t>();
+    ga.samples = samples;
+    ga.row_ptr = c->tr.row_ptr.as<int64_t>();
+    ga.col = c->tr.col.as<int32_t>();
+    ga.val = c->tr.val.as<double>();
+    ga.K = c->K_loc;
+    ga.H = c->P.local_iters;
+    ga.nbatch = c->nbatch;
+    ga.gt = gt;
+    ga.prof = c->sa.prof ? c->sa.prof + (size_t)c->K_loc * 32 : nullptr;  // phase sums of this launch
+    return ga;
+}
+
 // fuse_apply: w += sum * mult inside the fold (one rank, no exchange).
 // chain_init: strict multi-rank fold, continuing the previous ranks' fold.
 static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* chain_init = nullptr) {
@@ -736,13 +795,33 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         c->zero_owed = -1;
     }
     if (H >= 1) {
-        c->timed(COCOA_K_SAMPLE, [&] {
-            launch_sampler(c->part_ptr.as<int64_t>(), K, seed, H, c->samples.as<int32_t>(), c->jump.as<uint64_t>(), s);
-        });
+        // (samples, Gram rows) of this round: prefetched during the last round's
+        // solver (overlap), else computed here
+        const bool gram_rows = c->use_gram && c->method != COCOA_METHOD_MBCD;
+        const bool overlap = gram_rows && c->gstream && c->gt2.p;
+        int b = 0;
+        if (overlap && c->pre_t == t) {
+            b = c->pre_buf;
+            HIPCHK(hipStreamWaitEvent(s, c->g_ready, 0));
+        } else {
+            if (c->pre_t >= 0) HIPCHK(hipStreamWaitEvent(s, c->g_ready, 0));  // a prefetch of another round: done first
+            c->timed(COCOA_K_SAMPLE, [&] {
+                launch_sampler(c->part_ptr.as<int64_t>(), K, seed, H, c->samples.as<int32_t>(), c->jump.as<uint64_t>(), s);
+            });
+            if (gram_rows) {
+                GramArgs ga = gram_args(c, c->samples.as<int32_t>(), c->gt.as<double>());
+                if (ga.prof) HIPCHK(hipMemsetAsync(ga.prof, 0, 8 * sizeof(uint64_t), s));
+                c->timed(COCOA_K_GRAM, [&] { launch_gram(ga, s); });
+            }
+        }
+        c->pre_t = -1;
+        int32_t* smp = b ? c->samples2.as<int32_t>() : c->samples.as<int32_t>();
+        double* gtb = b ? c->gt2.as<double>() : c->gt.as<double>();
+        c->sa.samples = smp;
         if (c->use_plan) {
             PlanArgs pa{};
             pa.part_ptr = c->part_ptr.as<int64_t>();
-            pa.samples = c->samples.as<int32_t>();
+            pa.samples = smp;
             pa.row_ptr = c->tr.row_ptr.as<int64_t>();
             pa.col = c->tr.col.as<int32_t>();
             pa.val = c->tr.val.as<double>();
@@ -768,22 +847,9 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             });
         }
         if (c->use_gram) {
-            if (c->method != COCOA_METHOD_MBCD) {
-                GramArgs ga{};
-                ga.part_ptr = c->part_ptr.as<int64_t>();
-                ga.samples = c->samples.as<int32_t>();
-                ga.row_ptr = c->tr.row_ptr.as<int64_t>();
-                ga.col = c->tr.col.as<int32_t>();
-                ga.val = c->tr.val.as<double>();
-                ga.K = K;
-                ga.H = H;
-                ga.nbatch = c->nbatch;
-                ga.gt = c->gt.as<double>();
-                c->timed(COCOA_K_GRAM, [&] { launch_gram(ga, s); });
-            }
             GramSolverArgs g{};
             g.part_ptr = c->part_ptr.as<int64_t>();
-            g.samples = c->samples.as<int32_t>();
+            g.samples = smp;
             g.plan_beg = c->plan_beg.as<int64_t>();
             g.plan_z = c->plan_z.as<int32_t>();
             g.plan_y = c->plan_y.as<double>();
@@ -794,7 +860,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.alpha = c->alpha.as<double>();
             g.alpha_work = c->alpha_work.as<double>();
             g.dw = dws;
-            g.gt = c->gt.p ? c->gt.as<double>() : nullptr;
+            g.gt = gram_rows ? gtb : nullptr;
             g.status = c->status.as<int>();
             g.prof = c->sa.prof;
             g.d = d;
@@ -806,6 +872,27 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.sigma = c->method == COCOA_METHOD_COCOA_PLUS ? c->sa.sigma : 1.0;
             g.scaling = c->scaling;
             c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(solver_mode(c->method), g, K, s); });
+            if (overlap) {
+                // round t+1's samples and Gram rows on gstream, beside this solver (its
+                // buffer's last reader, round t-1's solver, is done first)
+                HIPCHK(hipEventRecord(c->s_done[b], s));
+                const int nb = 1 - b;
+                if (t < c->P.num_rounds) {
+                    HIPCHK(hipStreamWaitEvent(c->gstream, c->s_done[nb], 0));
+                    int32_t* nsmp = nb ? c->samples2.as<int32_t>() : c->samples.as<int32_t>();
+                    double* ngt = nb ? c->gt2.as<double>() : c->gt.as<double>();
+                    const int32_t nseed = wrap32((int64_t)c->D.seed + t + 1);
+                    c->timed_on(c->gstream, COCOA_K_SAMPLE, [&] {
+                        launch_sampler(c->part_ptr.as<int64_t>(), K, nseed, H, nsmp, c->jump.as<uint64_t>(), c->gstream);
+                    });
+                    GramArgs ga = gram_args(c, nsmp, ngt);
+                    ga.prof = nullptr;
+                    c->timed_on(c->gstream, COCOA_K_GRAM, [&] { launch_gram(ga, c->gstream); });
+                    HIPCHK(hipEventRecord(c->g_ready, c->gstream));
+                    c->pre_t = t + 1;
+                    c->pre_buf = nb;
+                }
+            }
         } else if (is_sdca(c->method)) {
             c->timed(COCOA_K_SOLVER, [&] {
                 if (c->strict)
@@ -1473,7 +1560,7 @@ extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
     CAPI_BEGIN(ctx)
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     if (enable) {
-        ctx->prof.alloc_zero(sizeof(uint64_t) * (size_t)ctx->K_loc * 32, ctx->stream);
+        ctx->prof.alloc_zero(sizeof(uint64_t) * ((size_t)ctx->K_loc * 32 + 8), ctx->stream);  // + gram_kernel phases
         ctx->sa.prof = ctx->prof.as<uint64_t>();
     } else {
         ctx->sa.prof = nullptr;
@@ -1484,7 +1571,7 @@ extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
 extern "C" int cocoa_solver_profile_read(cocoa_ctx* ctx, uint64_t* out, int64_t count) {
     CAPI_BEGIN(ctx)
     require(out && ctx->prof.p, COCOA_E_STATE, "solver profiling not enabled");
-    const size_t n = std::min<size_t>((size_t)count, (size_t)ctx->K_loc * 32);
+    const size_t n = std::min<size_t>((size_t)count, (size_t)ctx->K_loc * 32 + 8);
     HIPCHK(hipMemcpyAsync(out, ctx->prof.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     CAPI_END(ctx)

@@ -109,9 +109,10 @@ struct GramArgs {
     const int64_t* row_ptr;
     const int32_t* col;
     const double* val;
-    int32_t K, H, nbatch;     // nbatch = ceil(H / 32)
+    int32_t K, H, nbatch;     // nbatch = ceil(H / 16)
     int32_t pad;
-    double* gt;               // [K][nbatch * 32][64]
+    double* gt;               // [K][nbatch * 16][64]
+    uint64_t* prof;           // optional [8] phase cycles summed over the workgroups (diagnostics)
 };
 
 struct GramSolverArgs {

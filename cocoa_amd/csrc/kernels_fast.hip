@@ -50,12 +50,15 @@ static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s) {
     GramSolverArgs g = a;
     size_t lds = gram_solver_lds(a.d, &g.hot);
-    if (const char* e = getenv("COCOA_GRAM_HOT")) {  // diagnostics: cap the LDS-resident columns
+#ifdef COCOA_DIAG
+    // diagnostic builds only (make diag): timing experiments, results invalid with DIAG
+    if (const char* e = getenv("COCOA_GRAM_HOT")) {  // cap the LDS-resident columns
         const int32_t h = std::min<int32_t>(g.hot, (int32_t)atoi(e) & ~63);
         lds -= sizeof(double) * (size_t)(g.hot - h);
         g.hot = h;
     }
-    if (const char* e = getenv("COCOA_GRAM_DIAG")) g.diag = atoi(e);  // timing experiments: results invalid
+    if (const char* e = getenv("COCOA_GRAM_DIAG")) g.diag = atoi(e);
+#endif
     if (mode == MODE_PLUS) launch_sg<MODE_PLUS>(g, grid, lds, s);
     else if (mode == MODE_COCOA) launch_sg<MODE_COCOA>(g, grid, lds, s);
     else launch_sg<MODE_MBCD>(g, grid, lds, s);

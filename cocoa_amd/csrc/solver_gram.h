@@ -49,6 +49,12 @@
 #include "kernels.h"
 #include "wave.h"
 
+#ifdef COCOA_DIAG
+#define COCOA_DIAG_ON 1  // diagnostic build: GramSolverArgs::diag may skip work (timing only)
+#else
+#define COCOA_DIAG_ON 0
+#endif
+
 namespace cocoa {
 
 constexpr int kGB = 16;                  // steps per batch
@@ -101,205 +107,217 @@ __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70);
 __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F); }  // lgkmcnt(0)
 
 // ================================================================ Gram ==
-// Gt[k][j][slot] = x_{s} . x_j for the step s of window slot `slot` in j's
+// Gt[k][j][slot] = x_s . x_j for the step s of window slot `slot` in j's
 // window [16 floor(j/16), +64) with s > j; 0 otherwise.
-// One workgroup per (partition, batch of 16 updaters): partners are the 64
-// steps of the window.  Hot columns (device index < kGHot) go through a dense
-// LDS image of the partners (lanes = partners, one LDS read per hot entry of
-// the updater); the other columns through an LDS hash of the partners' cold
-// entries (lanes = the updater's entries, a probe each).
-constexpr int kGramTable = 8192;     // hash slots (power of two, >= 2 x kGramCap: probes stay short)
-constexpr int kGramCap = 4096;       // packed partner positions per pass (their cold entries are inserted)
+// One workgroup per (partition, batch of 16 updaters); its 64 partners are the
+// steps of the window (the updaters are partners 0..15).  The window's
+// entries are packed partner by partner and loaded at once (256 per unit, up
+// to kGramNU units in registers, owners found branch-free): one round trip to
+// memory instead of one per row.  Then
+//   hot columns (device index < kGHot, the most frequent): a dense image
+//     XP[p][c] of the 64 partners; G_hot = XP[0..15] XP^T with lanes =
+//     partners and the updater values broadcast from LDS;
+//   cold columns: an LDS hash (column -> list of (updater, value)) of the
+//     updaters' cold entries, filled tile by tile (kGramTile packed positions
+//     of the updater rows at a time); every partner cold entry probes it.
+// Windows longer than the register chunk reload it per tile (same results).
+constexpr int kGramTable = 2048;     // hash slots (power of two, 2 x kGramTile)
+constexpr int kGramTile = 1024;      // updater positions per hash tile
+constexpr int kGramNU = 24;          // 256-entry units in registers
+constexpr int kGramCH = kGramNU * 256;
+constexpr int kGHotS = kGHot + 1;    // XP row stride (doubles)
 
 struct GramLds {
-    double X[kGSlots][kGHot + 1];    // +1: partner rows start on different banks
-    double acc[kGB][kGSlots];        // G of the block's updaters
+    double XP[kGSlots][kGHotS];      // hot image of the partners (updaters = rows 0..15)
+    double acc[kGB][kGSlots];        // G of the updaters against the window
     int32_t tkey[kGramTable];
     int32_t thead[kGramTable];
-    double eval[kGramCap];
-    int16_t enext[kGramCap];
-    int8_t epart[kGramCap];
+    double eval[kGramTile];
+    int16_t enext[kGramTile];
+    int8_t eu[kGramTile];
     int64_t pbeg[kGSlots];
-    int32_t pz[kGSlots];
-    int32_t pcum[kGSlots + 1];
+    int32_t pcum[kGSlots + 1];       // packed offsets of the partners
 };
-static_assert(sizeof(GramLds) <= 160 * 1024, "gram_kernel LDS");
+static_assert(sizeof(GramLds) <= 80 * 1024, "gram_kernel LDS: two workgroups per CU");
 
-__device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 19; }  // 13 bits
+__device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 21; }  // 11 bits
 
-constexpr int kGramGU = 8;    // 256-position units each thread keeps in flight while staging
-constexpr int kGramUC = 2;    // register chunks (64 entries) per updater row; longer rows loop
-
-__global__ __launch_bounds__(256, 1) void gram_kernel(GramArgs a) {
+__global__ __launch_bounds__(256, 2) void gram_kernel(GramArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramLds& L = *(GramLds*)lds_raw;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int k = blockIdx.x % a.K;
-    const int g = blockIdx.x / a.K;
+    uint64_t tph = a.prof ? __builtin_readcyclecounter() : 0;
+    auto phase = [&](int i) {  // diagnostics: thread 0 adds the phase's cycles
+        if (a.prof && tid == 0) {
+            const uint64_t t = __builtin_readcyclecounter();
+            atomicAdd((unsigned long long*)&a.prof[i], (unsigned long long)(t - tph));
+            tph = t;
+        }
+    };
+    // XCD-aware order: blocks land on the 8 XCDs round robin; one partition's
+    // consecutive batches (3/4 of their partners shared) stay on one XCD, close
+    // in time, so its L2 serves the re-reads
+    int k, g;
+    {
+        const int64_t b = blockIdx.x;
+        if (a.K % 8 == 0) {
+            const int64_t kx = a.K / 8, i = b / 8;
+            k = (int)((b % 8) + 8 * (i % kx));
+            g = (int)(i / kx);
+        } else {
+            k = (int)(b % a.K);
+            g = (int)(b / a.K);
+        }
+    }
     const int32_t H = a.H;
     const int32_t j0 = g * kGB;
     const int32_t P = min(kGSlots, H - j0);     // partners [j0, j0 + P)
-    const int32_t U = min(kGB, H - j0);          // updaters [j0, j0 + U) = partners [0, U)
+    const int32_t U = min(kGB, H - j0);          // updaters = partners [0, U)
     const int64_t p0 = a.part_ptr[k];
     const int32_t* smp = a.samples + (size_t)k * H;
-    // partner rows
-    if (tid < kGSlots) {
+    if (wv == 0) {
         int64_t b = 0;
         int32_t z = 0;
-        if (tid < P) {
-            const int64_t r = p0 + smp[j0 + tid];
+        if (lane < P) {
+            const int64_t r = p0 + smp[j0 + lane];
             b = a.row_ptr[r];
             z = (int32_t)(a.row_ptr[r + 1] - b);
         }
-        L.pbeg[tid] = b;
-        L.pz[tid] = z;
-    }
-    for (int i = tid; i < kGSlots * (kGHot + 1); i += 256) (&L.X[0][0])[i] = 0.0;
-    for (int i = tid; i < kGB * kGSlots; i += 256) (&L.acc[0][0])[i] = 0.0;
-    __syncthreads();
-    if (wv == 0) {
-        const int32_t inc = wave_incl_scan(L.pz[lane]);
+        const int32_t inc = wave_incl_scan(z);
+        L.pbeg[lane] = b;
         L.pcum[lane + 1] = inc;
         if (lane == 0) L.pcum[0] = 0;
     }
+    for (int i = tid; i < kGSlots * kGHotS; i += 256) (&L.XP[0][0])[i] = 0.0;
+    for (int i = tid; i < kGB * kGSlots; i += 256) (&L.acc[0][0])[i] = 0.0;
     __syncthreads();
-    const int32_t T = L.pcum[kGSlots];
-    auto owner = [&](int32_t q) {  // partner whose entries hold packed position q: largest p, pcum[p] <= q
-        int lo = 0;
+    phase(0);
+    const int32_t T = L.pcum[P], Q16 = L.pcum[U];
+    // registers: a chunk of packed positions [qa, qa + kGramCH): column (-1 past
+    // T), value, owner partner (4 per word)
+    int32_t cc[kGramNU];
+    double vv[kGramNU];
+    uint32_t ow[kGramNU / 4];
+    int32_t reg_qa = -1;
+    auto load = [&](int32_t qa) {
+        if (reg_qa == qa) return;
+        reg_qa = qa;
+        int o[kGramNU];
 #pragma unroll
-        for (int st = kGSlots / 2; st >= 1; st >>= 1)
-            if (L.pcum[lo + st] <= q) lo += st;
-        return lo;
-    };
-    // this wave's updaters (u = wv + 4 i): first kGramUC chunks in registers,
-    // loads issued now so they land while the partner structures are built
-    constexpr int NU = kGB / 4;
-    int32_t uc[NU][kGramUC];
-    double uv[NU][kGramUC];
+        for (int u = 0; u < kGramNU; ++u) {  // owners: independent binary searches, interleaved
+            const int32_t q = min(qa + u * 256 + tid, T - 1);
+            int lo = 0;
 #pragma unroll
-    for (int i = 0; i < NU; ++i) {
-        const int u = wv + 4 * i;
-        const int64_t b = L.pbeg[u];
-        const int32_t z = u < U ? L.pz[u] : 0;
-#pragma unroll
-        for (int c = 0; c < kGramUC; ++c) {
-            const int32_t e = 64 * c + lane;
-            uc[i][c] = e < z ? a.col[b + e] : -1;
-            uv[i][c] = e < z ? a.val[b + e] : 0.0;
+            for (int st = kGSlots / 2; st >= 1; st >>= 1)
+                if (L.pcum[lo + st] <= q) lo += st;
+            o[u] = lo;
         }
+#pragma unroll
+        for (int u = 0; u < kGramNU; ++u) {
+            const int32_t q = qa + u * 256 + tid;
+            const bool ok = q < T;
+            const int64_t e = ok ? L.pbeg[o[u]] + (q - L.pcum[o[u]]) : 0;
+            cc[u] = ok ? a.col[e] : -1;
+            vv[u] = ok ? a.val[e] : 0.0;
+        }
+#pragma unroll
+        for (int w = 0; w < kGramNU / 4; ++w)
+            ow[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
+                    ((uint32_t)o[4 * w + 3] << 24);
+    };
+    auto owner_of = [&](int u) { return (int)((ow[u / 4] >> (8 * (u % 4))) & 0xFFu); };
+    load(0);
+    // hot image (duplicate columns of a row add up, as in the dot)
+    for (int32_t qa = 0; qa < T; qa += kGramCH) {
+        load(qa);
+#pragma unroll
+        for (int u = 0; u < kGramNU; ++u)
+            if (cc[u] >= 0 && cc[u] < kGHot) atomicAdd(&L.XP[owner_of(u)][cc[u]], vv[u]);
     }
-    // cold probe of one updater entry (col c >= kGHot, value v) against the table
-    auto probe = [&](int u, int32_t c, double v) {
-        uint32_t h = gram_hash(c) & (kGramTable - 1);
-        for (;;) {
-            const int32_t key = L.tkey[h];
-            if (key == c) {
-                for (int32_t i = L.thead[h]; i >= 0; i = L.enext[i]) {
-                    const int p = L.epart[i];
-                    if (p > u) atomicAdd(&L.acc[u][p], v * L.eval[i]);
-                }
-                return;
-            }
-            if (key == -1) return;
-            h = (h + 1) & (kGramTable - 1);
-        }
-    };
-    // passes of kGramCap packed partner positions: dense hot image of all
-    // positions, hashed cold entries of the pass, cold probes of the updaters
-    for (int32_t qa = 0; qa < T; qa += kGramCap) {
-        if (qa > 0) __syncthreads();  // the previous pass's probes are done with the table
+    phase(1);
+    // cold part, one hash tile of updater positions at a time
+    for (int32_t ta = 0; ta < Q16; ta += kGramTile) {
         for (int i = tid; i < kGramTable; i += 256) {
             L.tkey[i] = -1;
             L.thead[i] = -1;
         }
         __syncthreads();
-        const int32_t qb = min(T, qa + kGramCap);
-        for (int32_t q0 = qa; q0 < qb; q0 += 256 * kGramGU) {
-            int32_t cc[kGramGU];
-            double vv[kGramGU];
-            int pp[kGramGU];
+        const int32_t tb = min(Q16, ta + kGramTile);
+        for (int32_t qa = (ta / kGramCH) * kGramCH; qa < tb; qa += kGramCH) {
+            load(qa);
 #pragma unroll
-            for (int u = 0; u < kGramGU; ++u) {
-                const int32_t q = q0 + 256 * u + tid;
-                cc[u] = -1;
-                vv[u] = 0.0;
-                pp[u] = 0;
-                if (q < qb) {
-                    const int p = owner(q);
-                    const int64_t e = L.pbeg[p] + (q - L.pcum[p]);
-                    pp[u] = p;
-                    cc[u] = a.col[e];
-                    vv[u] = a.val[e];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kGramGU; ++u) {
+            for (int u = 0; u < kGramNU; ++u) {
+                const int32_t q = qa + u * 256 + tid;
                 const int32_t c = cc[u];
-                if (c < 0) continue;
-                if (c < kGHot) {  // duplicate columns of a row add up, as in the dot
-                    atomicAdd(&L.X[pp[u]][c], vv[u]);
-                    continue;
+                if (q >= ta && q < tb && c >= kGHot) {
+                    const int32_t i = q - ta;
+                    L.eval[i] = vv[u];
+                    L.eu[i] = (int8_t)owner_of(u);
+                    uint32_t h = gram_hash(c) & (kGramTable - 1);
+                    for (;;) {
+                        const int32_t old = atomicCAS(&L.tkey[h], -1, c);
+                        if (old == -1 || old == c) break;
+                        h = (h + 1) & (kGramTable - 1);
+                    }
+                    L.enext[i] = (int16_t)atomicExch(&L.thead[h], i);
                 }
-                const int32_t i = q0 + 256 * u + tid - qa;
-                L.epart[i] = (int8_t)pp[u];
-                L.eval[i] = vv[u];
-                uint32_t h = gram_hash(c) & (kGramTable - 1);
-                for (;;) {
-                    const int32_t old = atomicCAS(&L.tkey[h], -1, c);
-                    if (old == -1 || old == c) break;
-                    h = (h + 1) & (kGramTable - 1);
-                }
-                L.enext[i] = (int16_t)atomicExch(&L.thead[h], i);
             }
         }
         __syncthreads();
+        phase(5);
+        for (int32_t qa = 0; qa < T; qa += kGramCH) {
+            load(qa);
 #pragma unroll
-        for (int i = 0; i < NU; ++i) {
-            const int u = wv + 4 * i;
-            if (u >= U) continue;
-#pragma unroll
-            for (int c = 0; c < kGramUC; ++c)
-                if (uc[i][c] >= kGHot) probe(u, uc[i][c], uv[i][c]);
-            const int64_t b = L.pbeg[u];
-            const int32_t z = L.pz[u];
-            for (int32_t e = 64 * kGramUC + lane; e < z; e += 64) {  // rows past the register chunks
-                const int32_t c = a.col[b + e];
-                if (c >= kGHot) probe(u, c, a.val[b + e]);
+            for (int u = 0; u < kGramNU; ++u) {
+                const int32_t c = cc[u];
+                if (c < kGHot) continue;
+                const int pp = owner_of(u);
+                if (pp == 0) continue;  // no updater before partner 0
+                uint32_t h = gram_hash(c) & (kGramTable - 1);
+                for (;;) {
+                    const int32_t key = L.tkey[h];
+                    if (key == c) {
+                        for (int32_t i = L.thead[h]; i >= 0; i = L.enext[i]) {
+                            const int uu = L.eu[i];
+                            if (pp > uu) atomicAdd(&L.acc[uu][pp], vv[u] * L.eval[i]);
+                        }
+                        break;
+                    }
+                    if (key == -1) break;
+                    h = (h + 1) & (kGramTable - 1);
+                }
             }
         }
+        __syncthreads();
+        phase(6);
     }
-    __syncthreads();  // X complete, cold contributions in acc
-    // hot part: lanes = partners, one LDS read per hot entry of the updater
-#pragma unroll
-    for (int i = 0; i < NU; ++i) {
-        const int u = wv + 4 * i;
-        if (u >= U) continue;
-        double acc = 0.0;
-        auto hot = [&](int32_t c, double v) {
-            uint64_t m = __ballot(c >= 0 && c < kGHot);
-            while (m) {
-                const int src = __builtin_ctzll(m);
-                m &= m - 1;
-                const int32_t cc = __builtin_amdgcn_readlane(c, src);
-                acc = fma(readlane_d(v, src), L.X[lane][cc], acc);
-            }
-        };
-#pragma unroll
-        for (int c = 0; c < kGramUC; ++c) hot(uc[i][c], uv[i][c]);
-        const int64_t b = L.pbeg[u];
-        const int32_t z = L.pz[u];
-        for (int32_t e0 = 64 * kGramUC; e0 < z; e0 += 64) {
-            const int32_t e = e0 + lane;
-            hot(e < z ? a.col[b + e] : -1, e < z ? a.val[b + e] : 0.0);
+    phase(2);
+    // hot part: wave wv -> updaters 4 wv .. 4 wv + 3, lane = partner
+    {
+        double h0 = 0.0, h1 = 0.0, h2 = 0.0, h3 = 0.0;
+        const int u0 = 4 * wv;
+#pragma unroll 8
+        for (int c = 0; c < kGHot; ++c) {
+            const double xp = L.XP[lane][c];
+            h0 = fma(L.XP[u0][c], xp, h0);
+            h1 = fma(L.XP[u0 + 1][c], xp, h1);
+            h2 = fma(L.XP[u0 + 2][c], xp, h2);
+            h3 = fma(L.XP[u0 + 3][c], xp, h3);
         }
-        L.acc[u][lane] += acc;  // this wave owns row u; its cold atomics are done (barrier above)
+        L.acc[u0][lane] += h0;  // sole writer of (u, lane) now
+        L.acc[u0 + 1][lane] += h1;
+        L.acc[u0 + 2][lane] += h2;
+        L.acc[u0 + 3][lane] += h3;
     }
+    __syncthreads();
+    phase(3);
     // Gt rows of the block's updaters: slot of partner p = (j0 + p) & 63
     double* out = a.gt + ((size_t)k * a.nbatch * kGB + j0) * kGSlots;
     for (int u = wv; u < kGB; u += 4) {
         const double v = (u < U && lane > u && lane < P) ? L.acc[u][lane] : 0.0;
         __builtin_nontemporal_store(v, out + (size_t)u * kGSlots + ((j0 + lane) & (kGSlots - 1)));
     }
+    phase(4);
 }
 
 // ============================================================== solver ==
@@ -648,7 +666,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int t = 0; t < 8; ++t)
-                            if (cc[t] != 0.0 && !(a.diag & 1)) dw_add(cl[t], vl[t] * cc[t]);
+                            if (cc[t] != 0.0 && !(COCOA_DIAG_ON && (a.diag & 1))) dw_add(cl[t], vl[t] * cc[t]);
                     }
                 } else {
                     // a batch too long to stage: straight from the CSR, row by row
@@ -703,7 +721,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                                 const int32_t c = rw[t] < kGB ? cl[t] : -1;
                                 // a hot (LDS) or empty lane loads the constant 1 -- one register
                                 // never mixes a global load with an LDS read (that would serialise)
-                                if (!(a.diag & 2)) dw[u] = dw_load(c >= hot ? dwk + c : &g_gram_one);
+                                if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(c >= hot ? dwk + c : &g_gram_one);
                                 hx[t] = hotl[(c >= 0 && c < hot) ? c : 0];
                             }
                             __builtin_amdgcn_sched_barrier(0);  // all reads of the group out before the products

@@ -227,11 +227,14 @@ class Engine:
     def solver_profile(self, on=True):
         C.check(C.lib().cocoa_solver_profile(self.h, 1 if on else 0), self.h)
 
-    def solver_profile_read(self):
-        out = np.zeros(self.K_loc * 32, np.uint64)
+    def solver_profile_read(self, count=None):
+        """Raw counters: [K_loc][32] of the solver, then (count > 32 K_loc) the
+        gram_kernel phase sums.  Default: the solver part as [K_loc][2][16]."""
+        n = self.K_loc * 32 if count is None else count
+        out = np.zeros(n, np.uint64)
         C.check(C.lib().cocoa_solver_profile_read(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                                   len(out)), self.h)
-        return out.reshape(self.K_loc, 2, 16)
+        return out.reshape(self.K_loc, 2, 16) if count is None else out
 
     def plan(self):
         buf = ctypes.create_string_buffer(1024)

@@ -26,7 +26,11 @@ def main():
         e.round(t)
     e.sync()
     st = e.kernel_stats()
-    full = e.solver_profile_read().reshape(e.K_loc, 32).astype(np.float64)
+    allp = e.solver_profile_read(e.K_loc * 32 + 8).astype(np.float64)
+    full = allp[:e.K_loc * 32].reshape(e.K_loc, 32)
+    nwg = e.K_loc * ((sh.H + 15) // 16)
+    gram_phases = dict(zip(["meta_zero", "load_hot_image", "-", "hot_product", "store", "cold_insert", "cold_probe", "-"],
+                           (allp[e.K_loc * 32:e.K_loc * 32 + 8] / nwg).tolist()))
     raw = full[:, :16].reshape(e.K_loc, 4, 4)
     mem = full[:, 16:20].mean(axis=0)
     roles = ["chain", "memory", "loader", "fetch0"]
@@ -36,7 +40,8 @@ def main():
                      for i, r in enumerate(roles)},
            "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
            "memory_phases_cyc_per_batch": dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
-                                                   (mem / ((sh.H + 15) // 16)).tolist()))}
+                                                   (mem / ((sh.H + 15) // 16)).tolist())),
+           "gram_phase_cyc_per_wg": gram_phases}
     print(json.dumps(out))
 
 
