@@ -28,8 +28,8 @@ OBJS := $(BUILD)/kernels_strict.strict.o $(BUILD)/kernels_fast.fast.o $(BUILD)/e
 $(OUT): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lpthread -ldl
 
-cocoa_amd/cocoa_driver: $(CSRC)/driver_main.cpp $(OUT) include/cocoa_capi.h
-	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude -x c++ $< -o $@ -Lcocoa_amd -lcocoa_hip -Wl,-rpath,'$$ORIGIN'
+cocoa_amd/cocoa_driver: $(CSRC)/driver_main.cpp $(CSRC)/jdouble.h $(OUT) include/cocoa_capi.h
+	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude -I$(CSRC) -x c++ $< -o $@ -Lcocoa_amd -lcocoa_hip -Wl,-rpath,'$$ORIGIN'
 
 # diagnostic build with per-step phase stamps in the local solver
 DIAG := build/diag

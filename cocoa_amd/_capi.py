@@ -122,6 +122,7 @@ SIGNATURES = {
     "cocoa_gen_synthetic": (_int, [_i32, _i64, _i32, _f64, _i32, ctypes.c_uint64, _i64, _i32,
                                     ctypes.POINTER(Dataset)]),
     "cocoa_dataset_free": (None, [ctypes.POINTER(Dataset)]),
+    "cocoa_java_double_string": (_int, [ctypes.c_double, ctypes.c_char_p, _i32]),
     "cocoa_jrandom_ints": (_int, [_i64, _i32, _i32, _pi32]),
     "cocoa_set_solver": (_int, [_vp, _int]),
     "cocoa_comm_unique_id": (_int, [_int, ctypes.c_char_p]),

@@ -20,6 +20,7 @@
 
 #include "../../include/cocoa_capi.h"
 #include "common.h"
+#include "jdouble.h"
 #include "jrandom.h"
 
 namespace cocoa {
@@ -485,5 +486,14 @@ extern "C" int cocoa_jrandom_ints(int64_t seed, int32_t bound, int32_t count, in
     if (!out || count < 0) return host_fail(COCOA_E_ARG, "cocoa_jrandom_ints: bad argument");
     JRandom r(seed);
     for (int32_t i = 0; i < count; ++i) out[i] = bound > 0 ? r.next_int(bound) : r.next(32);
+    return COCOA_OK;
+}
+
+// java.lang.Double.toString of the reference's JVM (JDK 7/8 FloatingDecimal)
+extern "C" int cocoa_java_double_string(double x, char* buf, int32_t cap) {
+    if (!buf || cap <= 0) return COCOA_E_ARG;
+    const std::string t = cocoa::jdouble::to_string(x);
+    if ((int32_t)t.size() + 1 > cap) return COCOA_E_ARG;
+    std::memcpy(buf, t.c_str(), t.size() + 1);
     return COCOA_OK;
 }

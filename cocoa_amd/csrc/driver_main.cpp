@@ -13,45 +13,12 @@
 #include <vector>
 
 #include "cocoa_capi.h"
+#include "jdouble.h"
 
 namespace {
 
-// java.lang.Double.toString with shortest round-trip digits
-std::string jstr(double x) {
-    if (std::isnan(x)) return "NaN";
-    if (std::isinf(x)) return x > 0 ? "Infinity" : "-Infinity";
-    if (x == 0.0) return std::signbit(x) ? "-0.0" : "0.0";
-    char buf[64];
-    int p = 1;
-    for (; p <= 17; ++p) {
-        std::snprintf(buf, sizeof buf, "%.*e", p - 1, std::fabs(x));
-        if (std::strtod(buf, nullptr) == std::fabs(x)) break;
-    }
-    // buf = d.ddddde[+-]XX
-    std::string s(buf);
-    const size_t epos = s.find('e');
-    std::string mant = s.substr(0, epos);
-    const int e10 = std::atoi(s.c_str() + epos + 1);
-    std::string digits;
-    for (char c : mant)
-        if (c != '.') digits += c;
-    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
-    std::string out = x < 0 ? "-" : "";
-    const double ax = std::fabs(x);
-    if (ax >= 1e-3 && ax < 1e7) {
-        std::string ip, fp;
-        if (e10 >= 0) {
-            ip = digits.substr(0, std::min<size_t>(digits.size(), (size_t)e10 + 1));
-            while ((int)ip.size() < e10 + 1) ip += '0';
-            fp = (int)digits.size() > e10 + 1 ? digits.substr((size_t)e10 + 1) : "0";
-        } else {
-            ip = "0";
-            fp = std::string((size_t)(-e10 - 1), '0') + digits;
-        }
-        return out + ip + "." + fp;
-    }
-    return out + digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0") + "E" + std::to_string(e10);
-}
+// java.lang.Double.toString as JDK 7/8 printed it (csrc/jdouble.h)
+std::string jstr(double x) { return cocoa::jdouble::to_string(x); }
 
 struct Bad : std::runtime_error {
     using std::runtime_error::runtime_error;

@@ -11,8 +11,6 @@ follow the Scala reference so a caller can switch over unchanged:
            printSummaryStatsPrimalDual / printSummaryStats   OptUtils.scala
   Params, DebugParams                             OptClasses.scala:21-42
 """
-import math
-from decimal import Decimal
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -20,31 +18,13 @@ import numpy as np
 
 from .data import LabeledData, load_libsvm
 from .engine import Engine
+from .jdouble import java_double_tostring
 
 
 def jstr(x):
-    """java.lang.Double.toString (shortest round-trip digits, as JDK >= 19)."""
-    x = float(x)
-    if x != x:
-        return "NaN"
-    if math.isinf(x):
-        return "Infinity" if x > 0 else "-Infinity"
-    if x == 0.0:
-        return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
-    sign = "-" if x < 0 else ""
-    t = Decimal(repr(abs(x))).as_tuple()
-    ds, e = "".join(map(str, t.digits)).lstrip("0"), t.exponent
-    while len(ds) > 1 and ds[-1] == "0":
-        ds, e = ds[:-1], e + 1
-    e10 = e + len(ds) - 1  # decimal exponent of the leading digit
-    if 1e-3 <= abs(x) < 1e7:
-        if e10 >= 0:
-            ip = ds[:e10 + 1].ljust(e10 + 1, "0")
-            fp = ds[e10 + 1:] or "0"
-        else:
-            ip, fp = "0", "0" * (-e10 - 1) + ds
-        return sign + ip + "." + fp
-    return sign + ds[0] + "." + (ds[1:] or "0") + "E" + str(e10)
+    """java.lang.Double.toString as the reference's JVM (JDK 7/8) printed it
+    (cocoa_amd/jdouble.py: sun.misc.FloatingDecimal restated)."""
+    return java_double_tostring(x)
 
 
 @dataclass

@@ -281,6 +281,12 @@ int cocoa_load_libsvm(const char *path, int32_t num_splits, int32_t num_features
 int cocoa_gen_synthetic(int32_t kind, int64_t n_rows, int32_t num_features, double mean_nnz, int32_t num_parts,
                         uint64_t seed, int64_t first_row, int32_t threads, cocoa_dataset *out);
 void cocoa_dataset_free(cocoa_dataset *ds);
+
+/* java.lang.Double.toString(x) as the reference's JVM (JDK 7/8,
+ * sun.misc.FloatingDecimal) printed it -- not always the shortest digits
+ * (2.0E23 -> "1.9999999999999998E23"); the driver's stdout lines use it.
+ * buf: at least 32 bytes. */
+int cocoa_java_double_string(double x, char *buf, int32_t cap);
 /* java.util.Random(seed).nextInt(bound) x count on the host (bound <= 0:
  * nextInt()). */
 int cocoa_jrandom_ints(int64_t seed, int32_t bound, int32_t count, int32_t *out);
