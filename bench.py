@@ -64,7 +64,7 @@ def main():
                          "(n rows, K = parts) whose partitions are split over the GPUs")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="rank exchange inside libcocoa_hip.so: RCCL over xGMI (one GPU per rank) or HOST (TCP)")
-    ap.add_argument("--solver", default="auto", choices=["auto", "gram", "chain"],
+    ap.add_argument("--solver", default="auto", choices=["auto", "gram", "chain", "dense"],
                     help="fast-mode SDCA local solver (cocoa_set_solver)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)

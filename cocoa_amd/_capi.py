@@ -20,7 +20,7 @@ METHOD_COCOA_PLUS, METHOD_COCOA, METHOD_MBCD, METHOD_MBSGD, METHOD_LOCALSGD = 0,
 METHODS = {"cocoa+": 0, "cocoa": 1, "mbcd": 2, "mbsgd": 3, "localsgd": 4}
 K_SAMPLE, K_SOLVER, K_FOLD, K_APPLY, K_EVAL, K_PLAN, K_GRAM = 0, 1, 2, 3, 4, 5, 6
 KERNEL_NAMES = ["sample", "solver", "fold", "apply", "eval", "plan", "gram"]
-SOLVERS = {"auto": 0, "chain": 1, "gram": 2}
+SOLVERS = {"auto": 0, "chain": 1, "gram": 2, "dense": 3}
 
 
 class CocoaError(RuntimeError):
@@ -90,6 +90,8 @@ SIGNATURES = {
     "cocoa_last_error": (ctypes.c_char_p, [_vp]),
     "cocoa_set_train": (_int, [_vp, _i32, _pi64, _pi64, _pi32, _pf64, _pf64, _i64, _i32, _i32, _i32]),
     "cocoa_set_test": (_int, [_vp, _pi64, _pi32, _pf64, _pf64, _i64]),
+    "cocoa_set_train_dense": (_int, [_vp, _i32, _pi64, _pf64, _pf64, _i64, _i32, _i32, _i32]),
+    "cocoa_set_test_dense": (_int, [_vp, _pf64, _pf64, _i64]),
     "cocoa_init": (_int, [_vp, ctypes.POINTER(Params), ctypes.POINTER(Debug), _int, _pf64]),
     "cocoa_round_local": (_int, [_vp, _i32]),
     "cocoa_dw_sum_device_ptr": (_int, [_vp, ctypes.POINTER(_vp)]),

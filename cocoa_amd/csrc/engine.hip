@@ -22,6 +22,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/cocoa_capi.h"
@@ -77,7 +78,22 @@ struct DevBuf {
 struct Csr {
     int64_t n = 0, nnz = 0;
     DevBuf row_ptr, col, val, y;
+    DevBuf col16;  // uint16 copy of col when d <= 65,536 (fast eval stream), else empty
 };
+
+// uint16 column copy for the fast eval when every device column fits 16 bits
+void upload_col16(DevBuf& b, const std::vector<int32_t>& pcol, int64_t nnz, int32_t d, hipStream_t s) {
+    if (d > 65536) {
+        b.free();
+        return;
+    }
+    std::vector<uint16_t> c16((size_t)std::max<int64_t>(nnz, 1));
+    for (int64_t q = 0; q < nnz; ++q) c16[(size_t)q] = (uint16_t)pcol[(size_t)q];
+    b.alloc(sizeof(uint16_t) * (size_t)nnz + 64);
+    HIPCHK(hipMemsetAsync((char*)b.p + sizeof(uint16_t) * (size_t)nnz, 0, 64, s));
+    if (nnz) HIPCHK(hipMemcpyAsync(b.p, c16.data(), sizeof(uint16_t) * (size_t)nnz, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // c16 is a local
+}
 
 constexpr size_t kLdsMax = 160 * 1024;
 constexpr int kStreamCap = 2048;
@@ -116,10 +132,20 @@ struct cocoa_ctx {
     DevBuf sqn, rowflags, part_ptr;
     std::vector<int64_t> h_part_ptr;
     bool any_dup = false;
+    bool tr_dense = false;  // every row stores columns 0..d-1 in order (val = X[n][d])
+    // Compact deltaW slices (large K_loc * d, e.g. C4): partition k's slice holds
+    // only the U_k distinct columns of its rows, in device order; the entries'
+    // slice positions are col_local.  fptr / fpos: for every device column j the
+    // flattened slice positions k * max_u + i holding it, in partition order
+    // (the fold's gather list).  Built by cocoa_set_train when K_loc * d * 8 >=
+    // 1 GiB; used by the fast Gram solver.
+    bool compact_ready = false, dw_compact = false;
+    int64_t max_u = 0, sum_u = 0;
+    DevBuf col_local, fptr, fpos;
     int32_t max_nl = 0, min_nl = 0;
     // test data (this rank)
     Csr te;
-    bool has_test = false;
+    bool has_test = false, te_dense = false;
     // row tiles of the fast evaluation pass (kEvalTile entries)
     DevBuf tiles, t_tiles;
     int64_t n_tiles = 0, n_t_tiles = 0;
@@ -156,6 +182,7 @@ struct cocoa_ctx {
     // Gram-window solver (fast SDCA methods on sparse rows, solver_gram.h)
     int solver_kind = COCOA_SOLVER_AUTO;
     bool use_gram = false;
+    bool use_dense = false;  // dense-row local solver (solver_dense.h)
     DevBuf gt, status;  // status: set by a Gram-solver launch whose hand-off timed out
     int32_t nbatch = 0;
     // Round t+1's samples and Gram rows are computed on gstream while round t's
@@ -393,7 +420,128 @@ static void check_csr(const int64_t* row_ptr, const int32_t* col, int64_t n, int
                                            " outside [0," + std::to_string(d) + ")");
 }
 
+// Rows that store every feature in index order: row r = columns 0..d-1 at
+// entries [r d, (r + 1) d), so the value array is the row-major matrix.
+static bool is_dense(const int64_t* row_ptr, const int32_t* col, int64_t n, int32_t d) {
+    if (n < 1) return false;
+    for (int64_t r = 0; r <= n; ++r)
+        if (row_ptr[r] != r * (int64_t)d) return false;
+    for (int64_t r = 0; r < n; ++r) {
+        const int32_t* c = col + r * (int64_t)d;
+        for (int32_t j = 0; j < d; ++j)
+            if (c[j] != j) return false;
+    }
+    return true;
+}
+
+// CSR view of a dense matrix (the column array is the only new storage)
+static void dense_csr(int64_t n, int32_t d, std::vector<int64_t>& rp, std::vector<int32_t>& col) {
+    rp.resize((size_t)n + 1);
+    for (int64_t r = 0; r <= n; ++r) rp[(size_t)r] = r * (int64_t)d;
+    col.resize((size_t)std::max<int64_t>(n * (int64_t)d, 1));
+    for (int64_t r = 0; r < n; ++r)
+        for (int32_t j = 0; j < d; ++j) col[(size_t)(r * (int64_t)d + j)] = j;
+}
+
+// Compact deltaW layout (see cocoa_ctx::compact_ready).  COCOA_DW_COMPACT=0 / 1
+// forces it off / on (tests); on by default once K_loc * d * 8 >= 1 GiB and the
+// distinct columns per partition are fewer than d / 4.
+static void build_compact(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* pcol) {
+    c->compact_ready = false;
+    c->col_local.free();
+    c->fptr.free();
+    c->fpos.free();
+    const int K = c->K_loc;
+    const int64_t d = c->d;
+    const char* env = std::getenv("COCOA_DW_COMPACT");
+    if (env ? std::atoi(env) == 0 : (size_t)K * (size_t)d * sizeof(double) < ((size_t)1 << 30)) return;
+    const int64_t nnz = c->tr.nnz;
+    std::vector<int32_t> cl((size_t)std::max<int64_t>(nnz, 1));
+    std::vector<std::vector<int32_t>> lists((size_t)K);
+    const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int tix = 0; tix < T; ++tix)
+        th.emplace_back([&, tix] {
+            std::vector<int32_t> mark((size_t)d, -1), idx((size_t)d, 0);
+            for (int k = tix; k < K; k += T) {
+                const int64_t q0 = row_ptr[c->h_part_ptr[(size_t)k]], q1 = row_ptr[c->h_part_ptr[(size_t)k + 1]];
+                std::vector<int32_t>& L = lists[(size_t)k];
+                for (int64_t q = q0; q < q1; ++q) {
+                    const int32_t j = pcol[q];
+                    if (mark[(size_t)j] != k) mark[(size_t)j] = k, L.push_back(j);
+                }
+                std::sort(L.begin(), L.end());  // device order: adjacent columns, adjacent positions
+                for (size_t i = 0; i < L.size(); ++i) idx[(size_t)L[i]] = (int32_t)i;
+                for (int64_t q = q0; q < q1; ++q) cl[(size_t)q] = idx[(size_t)pcol[q]];
+            }
+        });
+    for (auto& t : th) t.join();
+    int64_t mu = 1, su = 0;
+    for (auto& L : lists) mu = std::max<int64_t>(mu, (int64_t)L.size()), su += (int64_t)L.size();
+    if (!env && mu * 4 > d) return;  // not sparse enough per partition to pay
+    if ((uint64_t)K * (uint64_t)mu >= ((uint64_t)1 << 32)) return;
+    std::vector<int64_t> fp((size_t)d + 1, 0);
+    for (auto& L : lists)
+        for (int32_t j : L) fp[(size_t)j + 1]++;
+    for (int64_t j = 0; j < d; ++j) fp[(size_t)j + 1] += fp[(size_t)j];
+    std::vector<uint32_t> pos((size_t)std::max<int64_t>(su, 1));
+    std::vector<int64_t> cur(fp.begin(), fp.end() - 1);
+    for (int k = 0; k < K; ++k) {  // partition order inside every column's list
+        const std::vector<int32_t>& L = lists[(size_t)k];
+        for (size_t i = 0; i < L.size(); ++i) pos[(size_t)cur[(size_t)L[i]]++] = (uint32_t)((uint64_t)k * mu + i);
+    }
+    hipStream_t s = c->stream;
+    upload_padded(c->col_local, cl.data(), sizeof(int32_t) * (size_t)nnz, s);
+    upload(c->fptr, fp.data(), sizeof(int64_t) * fp.size(), s);
+    upload(c->fpos, pos.data(), sizeof(uint32_t) * pos.size(), s);
+    HIPCHK(hipStreamSynchronize(s));
+    c->max_u = mu;
+    c->sum_u = su;
+    c->compact_ready = true;
+}
+
 // ------------------------------------------------------------------- data --
+extern "C" int cocoa_set_train_dense(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const double* X,
+                                     const double* y, int64_t n_rows, int32_t num_features, int32_t part_begin,
+                                     int32_t num_parts_global) {
+    if (!ctx) return COCOA_E_ARG;
+    if (!X || n_rows < 0 || num_features < 1) {
+        ctx->err = "cocoa_set_train_dense: bad argument";
+        cocoa_set_global_error(ctx->err);
+        return COCOA_E_ARG;
+    }
+    std::vector<int64_t> rp;
+    std::vector<int32_t> col;
+    try {
+        dense_csr(n_rows, num_features, rp, col);
+    } catch (const std::exception& e) {
+        ctx->err = std::string("cocoa_set_train_dense: ") + e.what();
+        cocoa_set_global_error(ctx->err);
+        return COCOA_E_ARG;
+    }
+    return cocoa_set_train(ctx, num_parts, part_ptr, rp.data(), col.data(), X, y, n_rows, num_features, part_begin,
+                           num_parts_global);
+}
+
+extern "C" int cocoa_set_test_dense(cocoa_ctx* ctx, const double* X, const double* y, int64_t n_rows) {
+    if (!ctx) return COCOA_E_ARG;
+    if (!X || n_rows < 0 || ctx->d < 1) {
+        ctx->err = ctx->d < 1 ? "cocoa_set_test_dense: call cocoa_set_train first" : "cocoa_set_test_dense: bad argument";
+        cocoa_set_global_error(ctx->err);
+        return ctx->d < 1 ? COCOA_E_STATE : COCOA_E_ARG;
+    }
+    std::vector<int64_t> rp;
+    std::vector<int32_t> col;
+    try {
+        dense_csr(n_rows, ctx->d, rp, col);
+    } catch (const std::exception& e) {
+        ctx->err = std::string("cocoa_set_test_dense: ") + e.what();
+        cocoa_set_global_error(ctx->err);
+        return COCOA_E_ARG;
+    }
+    return cocoa_set_test(ctx, rp.data(), col.data(), X, y, n_rows);
+}
+
 extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const int64_t* row_ptr,
                                const int32_t* col, const double* val, const double* y, int64_t n_rows,
                                int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
@@ -407,6 +555,7 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     for (int k = 0; k < num_parts; ++k) require(part_ptr[k + 1] >= part_ptr[k], COCOA_E_ARG, "part_ptr not monotone");
     check_csr(row_ptr, col, n_rows, num_features);
     const int64_t nnz = row_ptr[n_rows];
+    ctx->tr_dense = is_dense(row_ptr, col, n_rows, num_features);
     ctx->K_loc = num_parts;
     ctx->K_glob = num_parts_global;
     ctx->part_begin = part_begin;
@@ -473,12 +622,14 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     upload(ctx->d_inv, ctx->inv.data(), sizeof(int32_t) * (size_t)num_features, s);
     upload(ctx->tr.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
     upload_padded(ctx->tr.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
+    upload_col16(ctx->tr.col16, pcol, nnz, num_features, s);
     upload_padded(ctx->tr.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s);
+    build_compact(ctx, row_ptr, pcol.data());
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
     CAPI_END(ctx)
@@ -492,12 +643,14 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
     check_csr(row_ptr, col, n_rows, ctx->d);
     const int64_t nnz = row_ptr[n_rows];
     hipStream_t s = ctx->stream;
+    ctx->te_dense = is_dense(row_ptr, col, n_rows, ctx->d);
     ctx->te.n = n_rows;
     ctx->te.nnz = nnz;
     std::vector<int32_t> pcol((size_t)std::max<int64_t>(nnz, 1));
     for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];  // device feature order
     upload(ctx->te.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
     upload_padded(ctx->te.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
+    upload_col16(ctx->te.col16, pcol, nnz, ctx->d, s);
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s);
@@ -517,10 +670,11 @@ static int solver_mode(int m) {
 }
 static int32_t wrap32(int64_t x) { return (int32_t)(uint32_t)(uint64_t)x; }
 
-static void plan_solver(cocoa_ctx* c) {
+// vec_len: length of the solver's mutable vector (d, or the compact slice)
+static void plan_solver(cocoa_ctx* c, int64_t vec_len) {
     SolverArgs& a = c->sa;
     size_t off = 0;
-    const size_t vec_bytes = align16(sizeof(double) * (size_t)c->d);
+    const size_t vec_bytes = align16(sizeof(double) * (size_t)vec_len);
     // long rows (dense data, C3: 2,000 entries) would leave one row per batch and
     // make the loader's per-batch latency the bound: double the stream instead
     // (alpha then moves to HBM when it no longer fits; the chain prefetches it)
@@ -572,8 +726,9 @@ static bool dw_double_buffer(size_t bytes);
 
 extern "C" int cocoa_set_solver(cocoa_ctx* ctx, int kind) {
     CAPI_BEGIN(ctx)
-    require(kind == COCOA_SOLVER_AUTO || kind == COCOA_SOLVER_CHAIN || kind == COCOA_SOLVER_GRAM, COCOA_E_ARG,
-            "cocoa_set_solver: unknown solver");
+    require(kind == COCOA_SOLVER_AUTO || kind == COCOA_SOLVER_CHAIN || kind == COCOA_SOLVER_GRAM ||
+                kind == COCOA_SOLVER_DENSE,
+            COCOA_E_ARG, "cocoa_set_solver: unknown solver");
     ctx->solver_kind = kind;
     ctx->inited = false;  // takes effect at the next cocoa_init
     CAPI_END(ctx)
@@ -618,10 +773,19 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     ctx->gram_quiesce();                                            // no Gram prefetch in flight
     ctx->zpending[0] = ctx->zpending[1] = false;
     ctx->zero_owed = -1;
-    ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * d), s);
+    // the fast Gram solver on data with a compact layout: slices of max_u
+    // entries, re-zeroed by the fold as it reads them (no second set needed)
+    // CoCoA+ and MbCD (the chain or Gram solver, strict or fast) on data with a
+    // compact layout: slices of max_u entries, re-zeroed by the fold as it reads
+    // them (no second set).  CoCoA's task-local w copy is indexed by the global
+    // column, so CoCoA keeps the dense slices.
+    ctx->dw_compact = ctx->compact_ready && (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_MBCD) &&
+                      params->local_iters >= 1 && !(ctx->tr_dense && dense_solver_fits(d, ctx->max_nl));
+    const int64_t slice = ctx->dw_compact ? ctx->max_u : d;
+    ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * slice), s);
     // a second deltaW set only when it fits next to everything else (with 1 GiB
     // to spare); otherwise single buffering with the zero-in-fold path
-    ctx->dw_dbuf = dw_double_buffer((size_t)(K * d) * sizeof(double));
+    ctx->dw_dbuf = !ctx->dw_compact && dw_double_buffer((size_t)(K * d) * sizeof(double));
     if (ctx->dw_dbuf) {
         size_t free_b = 0, total_b = 0;
         HIPCHK(hipMemGetInfo(&free_b, &total_b));
@@ -639,7 +803,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     }
     const bool need_wloc = method == COCOA_METHOD_COCOA || method == COCOA_METHOD_LOCALSGD;
     ctx->method = method;
-    plan_solver(ctx);
+    plan_solver(ctx, slice);
     if (need_wloc && !(method == COCOA_METHOD_COCOA && ctx->vec_lds))
         ctx->wloc.alloc(sizeof(double) * (size_t)(K * d));
     else
@@ -654,7 +818,9 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
 
     SolverArgs& a = ctx->sa;
     a.row_ptr = ctx->tr.row_ptr.as<int64_t>();
-    a.col = ctx->tr.col.as<int32_t>();
+    // compact slices: the solvers index deltaW by the entry's slice position
+    // (x.w comes from the plan, which reads the global columns)
+    a.col = ctx->dw_compact ? ctx->col_local.as<int32_t>() : ctx->tr.col.as<int32_t>();
     a.val = ctx->tr.val.as<double>();
     a.y = ctx->tr.y.as<double>();
     a.sqn = ctx->sqn.as<double>();
@@ -666,7 +832,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.w = ctx->w.as<double>();
     a.dw = ctx->dw.as<double>();
     a.wloc = ctx->wloc.p ? ctx->wloc.as<double>() : nullptr;
-    a.d = d;
+    a.d = slice;
     a.H = H;
     a.any_dup = ctx->any_dup ? 1 : 0;
     a.raw_alpha = 0;
@@ -681,8 +847,21 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     // fast SDCA: the Gram-window solver, unless the rows are dense-long (C3:
     // 2,000 entries per row, where the chain solver streams w / deltaW from LDS)
     const double zavg = ctx->tr.n ? (double)ctx->tr.nnz / (double)ctx->tr.n : 0.0;
-    ctx->use_gram = !ctx->strict && is_sdca(method) && H >= 1 &&
-                    (ctx->solver_kind == COCOA_SOLVER_GRAM || (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0));
+    ctx->use_dense = !ctx->strict && is_sdca(method) && H >= 1 && ctx->tr_dense &&
+                     dense_solver_fits(d, ctx->max_nl) &&
+                     (ctx->solver_kind == COCOA_SOLVER_DENSE || ctx->solver_kind == COCOA_SOLVER_AUTO);
+    require(ctx->use_dense || ctx->solver_kind != COCOA_SOLVER_DENSE || ctx->strict || !is_sdca(method), COCOA_E_ARG,
+            "cocoa_init: the dense solver needs dense rows (cocoa_set_train_dense) with an even d <= 4096 and "
+            "partitions of at most 19,200 rows");
+    // AUTO takes the Gram solver when its side work has idle CUs to run on: at
+    // most one partition per CU (C2: 64 on 256 CUs).  With more partitions than
+    // CUs (C4 on one GPU: 1,024) every CU already runs chains and the Gram rows
+    // (measured: 46 ms per C4 round on the side stream) only compete with them.
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    ctx->use_gram = !ctx->strict && !ctx->use_dense && is_sdca(method) && H >= 1 &&
+                    (ctx->solver_kind == COCOA_SOLVER_GRAM ||
+                     (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0 && K <= ncu));
     if (ctx->use_gram) {
         ctx->status.alloc_zero(sizeof(int) * 4, s);
         ctx->nbatch = (H + 15) / 16;  // kGB = 16 steps per batch (solver_gram.h)
@@ -832,7 +1011,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             pa.H = H;
             // CoCoA's w moves inside the round: the chain solver forms x.w itself;
             // the Gram solver splits x.w_local = x.w + x.deltaW
-            pa.need_xw = c->method != COCOA_METHOD_COCOA || c->use_gram;
+            pa.need_xw = !c->use_dense && (c->method != COCOA_METHOD_COCOA || c->use_gram);
             pa.xw_cache = (c->xw_cached && !c->strict) ? c->row_xw.as<double>() : nullptr;
             pa.beg = c->plan_beg.as<int64_t>();
             pa.z = c->plan_z.as<int32_t>();
@@ -846,7 +1025,24 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
                     launch_plan_fast(pa, s);
             });
         }
-        if (c->use_gram) {
+        if (c->use_dense) {
+            DenseArgs g{};
+            g.X = c->tr.val.as<double>();
+            g.part_ptr = c->part_ptr.as<int64_t>();
+            g.samples = smp;
+            g.plan_y = c->plan_y.as<double>();
+            g.plan_q = c->plan_q.as<double>();
+            g.alpha = c->alpha.as<double>();
+            g.dw = dws;
+            g.w = c->w.as<double>();
+            g.d = d;
+            g.H = H;
+            g.lam_n = c->sa.lam_n;
+            g.inv_lam_n = 1.0 / c->sa.lam_n;
+            g.sigma = c->method == COCOA_METHOD_COCOA_PLUS ? c->sa.sigma : 1.0;
+            g.scaling = c->scaling;
+            c->timed(COCOA_K_SOLVER, [&] { launch_solver_dense(solver_mode(c->method), g, K, c->max_nl, s); });
+        } else if (c->use_gram) {
             GramSolverArgs g{};
             g.part_ptr = c->part_ptr.as<int64_t>();
             g.samples = smp;
@@ -855,7 +1051,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.plan_y = c->plan_y.as<double>();
             g.plan_q = c->plan_q.as<double>();
             g.plan_xw = c->plan_xw.as<double>();
-            g.col = c->tr.col.as<int32_t>();
+            g.col = c->dw_compact ? c->col_local.as<int32_t>() : c->tr.col.as<int32_t>();
             g.val = c->tr.val.as<double>();
             g.alpha = c->alpha.as<double>();
             g.alpha_work = c->alpha_work.as<double>();
@@ -863,7 +1059,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.gt = gram_rows ? gtb : nullptr;
             g.status = c->status.as<int>();
             g.prof = c->sa.prof;
-            g.d = d;
+            g.d = c->dw_compact ? c->max_u : d;  // slice length
             g.H = H;
             g.nbatch = c->nbatch;
             g.raw_alpha = 0;
@@ -923,8 +1119,12 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
     }
     if (chain_init) c->comm->chain_recv(c->dw_sum, d, true, s);  // the fold of ranks < rank (rank > 0)
     c->timed(COCOA_K_FOLD, [&] {
-        launch_fold(dws, K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, c->d_inv.as<int32_t>(),
-                    !c->dw_dbuf, s, chain_init);
+        if (c->dw_compact)
+            launch_fold_compact(dws, c->fptr.as<int64_t>(), c->fpos.as<uint32_t>(), d, c->dw_sum, c->w.as<double>(),
+                                c->mult, fuse_apply, c->d_inv.as<int32_t>(), s, chain_init);
+        else
+            launch_fold(dws, K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, c->d_inv.as<int32_t>(),
+                        !c->dw_dbuf, s, chain_init);
     });
     if (c->dw_dbuf) c->zero_owed = set;
     c->xw_cached = false;  // w moves this round (scale / fused apply / the caller's apply)
@@ -1107,6 +1307,8 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     e.n = ctx->tr.n;
     e.t_row_ptr = ctx->has_test ? ctx->te.row_ptr.as<int64_t>() : nullptr;
     e.t_col = ctx->has_test ? ctx->te.col.as<int32_t>() : nullptr;
+    e.col16 = ctx->tr.col16.p ? ctx->tr.col16.as<uint16_t>() : nullptr;
+    e.t_col16 = ctx->has_test && ctx->te.col16.p ? ctx->te.col16.as<uint16_t>() : nullptr;
     e.t_val = ctx->has_test ? ctx->te.val.as<double>() : nullptr;
     e.t_y = ctx->has_test ? ctx->te.y.as<double>() : nullptr;
     e.n_test = ctx->has_test ? ctx->te.n : 0;
@@ -1127,7 +1329,10 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
             launch_eval_strict(e, ctx->stream);
         else {
             e.row_xw = ctx->row_xw.as<double>();
-            launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
+            if (ctx->tr_dense && (!ctx->has_test || ctx->te_dense || ctx->te.n == 0) && dense_eval_fits(ctx->d))
+                launch_eval_dense(e, ctx->stream);  // rows read as X[n][d]: 8 B per entry
+            else
+                launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
             ctx->xw_cached = true;  // the next round's plan reuses these x.w (stream order)
         }
     });
@@ -1451,7 +1656,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     c.method = plus ? COCOA_METHOD_COCOA_PLUS : COCOA_METHOD_COCOA;
     const int32_t saved_max = c.max_nl;
     c.max_nl = nl;
-    plan_solver(&c);
+    plan_solver(&c, d);
     c.max_nl = saved_max;
     c.method = saved_method;
     DevBuf pp, smp, dwb, wb, wl, al, alw, sumb;
@@ -1511,7 +1716,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     if (!plus) ctx->to_host_order(wdev, w);
     if (delta_alpha)
         for (int32_t i = 0; i < nl; ++i) delta_alpha[i] = alpha[i] - old[(size_t)i];  // CoCoA.scala:190
-    if (ctx->inited) plan_solver(ctx);
+    if (ctx->inited) plan_solver(ctx, ctx->dw_compact ? ctx->max_u : d);
     CAPI_END(ctx)
 }
 
@@ -1583,10 +1788,12 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
     std::snprintf(buf, (size_t)len,
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
-                  "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\"}",
+                  "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
+                  "\"sum_u\":%lld}",
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,
-                  ctx->dw_dbuf ? 1 : 0, ctx->use_gram ? "gram" : "chain");
+                  ctx->dw_dbuf ? 1 : 0, ctx->use_dense ? "dense" : ctx->use_gram ? "gram" : "chain",
+                  ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u);
     CAPI_END(ctx)
 }

@@ -142,6 +142,24 @@ struct GramSolverArgs {
     double scaling;
 };
 
+// Dense-row local solver (solver_dense.h), fast mode: X is the CSR value array
+// of rows that store all d features in index order (row r at X + r * d)
+struct DenseArgs {
+    const double* X;          // rank-local rows, row-major [n][d]
+    const int64_t* part_ptr;
+    const int32_t* samples;   // K_loc * H
+    const double* plan_y;     // per step: y and ||x||^2 of the sampled row (plan kernel)
+    const double* plan_q;
+    double* alpha;            // persistent alpha: alphaOld in, the scaled update out
+    double* dw;               // K_loc * d private deltaW (every entry written)
+    const double* w;
+    int64_t d;
+    int32_t H, pad;
+    double lam_n, inv_lam_n;
+    double sigma;             // sigma' = K gamma (CoCoA+)
+    double scaling;
+};
+
 struct EvalArgs {
     // train side
     const int64_t* row_ptr;
@@ -174,6 +192,10 @@ struct EvalArgs {
     double* out;              // [4]: hinge_sum, alpha_sum, w_sq(norm^2 via sqrt), test_err_count
     double* row_scratch;      // n doubles (strict)
     double* row_xw;           // n doubles or null: eval v4 also stores each train row's x.w
+    // uint16 copies of col / t_col (device feature order) when d <= 65,536, or
+    // null; padded like col (the fast eval then streams 10 B per entry)
+    const uint16_t* col16;
+    const uint16_t* t_col16;
 };
 
 // fast translation unit
@@ -187,6 +209,11 @@ void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 size_t gram_solver_lds(int64_t d, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s);
+// dense rows: whether d and the largest partition (max_nl rows) fit the kernels
+bool dense_solver_fits(int64_t d, int64_t max_nl);
+bool dense_eval_fits(int64_t d);
+void launch_solver_dense(int mode, const DenseArgs& a, int grid, int64_t max_nl, hipStream_t s);
+void launch_eval_dense(const EvalArgs& a, hipStream_t s);
 
 // strict translation unit
 void launch_plan_strict(const PlanArgs& a, hipStream_t s);
@@ -200,6 +227,10 @@ void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H,
 void launch_zero(double* p, int64_t n, int blocks, hipStream_t s);
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
                  const int32_t* inv, bool zero, hipStream_t s, const double* init = nullptr);
+// compact deltaW slices: column j's sum is the gather of dw[fpos[fptr[j] ..
+// fptr[j+1])] in partition order (each entry re-zeroed as it is read)
+void launch_fold_compact(double* dw, const int64_t* fptr, const uint32_t* fpos, int64_t d, double* dw_sum, double* w,
+                         double mult, bool apply, const int32_t* inv, hipStream_t s, const double* init = nullptr);
 void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const int32_t* inv, hipStream_t s);
 void launch_scale(double* w, int64_t d, double scale, hipStream_t s);
 void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, double* out, hipStream_t s);

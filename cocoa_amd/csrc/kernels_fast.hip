@@ -6,6 +6,7 @@
 
 #include "kernels.h"
 #include "plan_impl.h"
+#include "solver_dense.h"
 #include "solver_gram.h"
 #include "solver_impl.h"
 #include "wave.h"
@@ -91,7 +92,20 @@ __device__ __forceinline__ double block_sum_n(double v, double* red) {
     return s;
 }
 
-template <int TILE, int BLOCK>
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+
+// 4 column indices at entry offset k: int32 (16 B) or, when d <= 65,536, the
+// uint16 copy (8 B: the stream drops from 12 to 10 B per entry)
+template <bool C16>
+__device__ __forceinline__ i32x4 load_cols(const int32_t* c32, const uint16_t* c16, int64_t k) {
+    if (C16) {
+        const u16x4 v = __builtin_nontemporal_load((const u16x4*)(c16 + k));
+        return i32x4{(int32_t)v.x, (int32_t)v.y, (int32_t)v.z, (int32_t)v.w};
+    }
+    return __builtin_nontemporal_load((const i32x4*)(c32 + k));
+}
+
+template <int TILE, int BLOCK, bool C16>
 __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     constexpr int UNITS = TILE / (4 * BLOCK);  // 4-entry units per thread (base alignment adds one)
     __shared__ double prod[TILE + 4];
@@ -108,6 +122,7 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
         const int64_t* te = tl + (test ? a.n_t_tiles : a.n_tiles) + 1;
         const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
         const int32_t* cl = test ? a.t_col : a.col;
+        const uint16_t* cl16 = test ? a.t_col16 : a.col16;
         const double* vl = test ? a.t_val : a.val;
         const double* yy = test ? a.t_y : a.y;
         const int64_t r0 = tl[tt], r1 = tl[tt + 1];
@@ -141,7 +156,7 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             v0[u] = f64x2{0.0, 0.0};
             v1[u] = v0[u];
             if (k < span) {
-                c[u] = __builtin_nontemporal_load((const i32x4*)(cl + base + k));
+                c[u] = load_cols<C16>(cl, cl16, base + k);
                 v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
                 v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
             }
@@ -213,8 +228,54 @@ int eval_fast_blocks(int64_t n_tiles, int64_t n_t_tiles) {
 }
 
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
-    eval_stream_kernel<kEvalTile, 512><<<blocks, 512, 0, s>>>(a);
+    if (a.col16 && (a.n_test == 0 || a.t_col16))
+        eval_stream_kernel<kEvalTile, 512, true><<<blocks, 512, 0, s>>>(a);
+    else
+        eval_stream_kernel<kEvalTile, 512, false><<<blocks, 512, 0, s>>>(a);
     eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+}
+
+// ------------------------------------------------------------ dense rows --
+// 16-byte column chunks per thread: CPT * 512 * 2 >= d
+static int dense_cpt(int64_t d) { return d <= 1024 ? 1 : d <= 2048 ? 2 : d <= 4096 ? 4 : 0; }
+
+bool dense_solver_fits(int64_t d, int64_t max_nl) {
+    return d >= 2 && (d & 1) == 0 && dense_cpt(d) > 0 && max_nl >= 1 && max_nl * 8 <= 150 * 1024;
+}
+bool dense_eval_fits(int64_t d) { return d >= 2 && (d & 1) == 0 && d <= 4096; }
+
+template <int MODE, int CPT, int P>
+static void launch_ds(const DenseArgs& a, int grid, size_t lds, hipStream_t s) {
+    (void)hipFuncSetAttribute((const void*)dense_solver_kernel<MODE, CPT, P>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dense_solver_kernel<MODE, CPT, P><<<grid, kDT, lds, s>>>(a);
+}
+
+template <int MODE>
+static void launch_ds_mode(const DenseArgs& a, int grid, size_t lds, hipStream_t s) {
+    // P = rows in flight per workgroup: 16 KB each at d = 2,000
+    switch (dense_cpt(a.d)) {
+        case 1: launch_ds<MODE, 1, 16>(a, grid, lds, s); break;
+        case 2: launch_ds<MODE, 2, 8>(a, grid, lds, s); break;
+        default: launch_ds<MODE, 4, 4>(a, grid, lds, s); break;
+    }
+}
+
+void launch_solver_dense(int mode, const DenseArgs& a, int grid, int64_t max_nl, hipStream_t s) {
+    const size_t lds = sizeof(double) * (size_t)max_nl;
+    if (mode == MODE_PLUS) launch_ds_mode<MODE_PLUS>(a, grid, lds, s);
+    else if (mode == MODE_COCOA) launch_ds_mode<MODE_COCOA>(a, grid, lds, s);
+    else launch_ds_mode<MODE_MBCD>(a, grid, lds, s);
+}
+
+void launch_eval_dense(const EvalArgs& a, hipStream_t s) {
+    constexpr int kBlocks = 1024;  // 4 per CU, one row per wave-iteration pair
+    const int64_t nch = a.d >> 1;
+    if (nch <= 256) eval_dense_kernel<4, 2><<<kBlocks, 256, 0, s>>>(a);
+    else if (nch <= 512) eval_dense_kernel<8, 2><<<kBlocks, 256, 0, s>>>(a);
+    else if (nch <= 1024) eval_dense_kernel<16, 2><<<kBlocks, 256, 0, s>>>(a);
+    else eval_dense_kernel<32, 1><<<kBlocks, 256, 0, s>>>(a);
+    eval_final_kernel<<<1, 256, 0, s>>>(a.partials, kBlocks, a.out);
 }
 
 }  // namespace cocoa

@@ -77,6 +77,24 @@ class Engine:
         C.check(C.lib().cocoa_set_test(self.h, C.i64p(data.row_ptr), C.i32p(data.col), C.f64p(data.val),
                                        C.f64p(data.y), data.n), self.h)
 
+    def set_train_dense(self, X, y, part_ptr, part_begin=0, num_parts_global=None):
+        """Dense rows (cocoa_set_train_dense): X float64 [n, d] row-major."""
+        X = np.ascontiguousarray(X, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        pp = np.ascontiguousarray(part_ptr, np.int64)
+        K = len(pp) - 1
+        Kg = K if num_parts_global is None else num_parts_global
+        C.check(C.lib().cocoa_set_train_dense(self.h, K, C.i64p(pp), C.f64p(X), C.f64p(y), X.shape[0], X.shape[1],
+                                              part_begin, Kg), self.h)
+        self.d = X.shape[1]
+        self.n_rows = X.shape[0]
+        self.K_loc, self.K_glob, self.part_begin = K, Kg, part_begin
+
+    def set_test_dense(self, X, y):
+        X = np.ascontiguousarray(X, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        C.check(C.lib().cocoa_set_test_dense(self.h, C.f64p(X), C.f64p(y), X.shape[0]), self.h)
+
     # -- ranks ---------------------------------------------------------------
     def comm_init(self, transport, rank, world, uid):
         """Attach a communicator (cocoa_comm_init): round / eval / run then
@@ -91,7 +109,7 @@ class Engine:
 
     # -- solver --------------------------------------------------------------
     def set_solver(self, kind):
-        """Fast-mode SDCA solver: "auto" (default), "chain" or "gram" (cocoa_set_solver)."""
+        """Fast-mode SDCA solver: "auto" (default), "chain", "gram" or "dense" (cocoa_set_solver)."""
         C.check(C.lib().cocoa_set_solver(self.h, C.SOLVERS[kind]), self.h)
 
     def init(self, method, n, num_rounds, local_iters, lam, beta=1.0, gamma=1.0, debug_iter=10, seed=0,

@@ -140,6 +140,18 @@ int cocoa_set_train(cocoa_ctx *ctx, int32_t num_parts, const int64_t *part_ptr, 
 /* This rank's share of DebugParams.testData (any row split). */
 int cocoa_set_test(cocoa_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *val, const double *y,
                    int64_t n_rows);
+/* Dense variants (epsilon-shaped data, config C3): X is row-major
+ * [n_rows][num_features] and every entry is a stored feature, as LIBSVM rows
+ * listing all d features in index order are (the reference's dot products then
+ * sum every entry in index order).  Equivalent to cocoa_set_train /
+ * cocoa_set_test with row r holding columns 0..d-1; cocoa_set_train also
+ * recognises such CSR input.  With dense rows, fast mode runs the dense local
+ * solver (deltaW and w in registers, 8 B per streamed entry) and the dense
+ * evaluation pass; strict mode keeps the stored-order CSR kernels. */
+int cocoa_set_train_dense(cocoa_ctx *ctx, int32_t num_parts, const int64_t *part_ptr, const double *X,
+                          const double *y, int64_t n_rows, int32_t num_features, int32_t part_begin,
+                          int32_t num_parts_global);
+int cocoa_set_test_dense(cocoa_ctx *ctx, const double *X, const double *y, int64_t n_rows);
 
 /* ---- solver ---------------------------------------------------------------*/
 /* Local solver of the SDCA methods in fast mode (strict mode always runs the
@@ -147,11 +159,14 @@ int cocoa_set_test(cocoa_ctx *ctx, const int64_t *row_ptr, const int32_t *col, c
  *   CHAIN -- each step gathers deltaW (or w) at its row and reduces the dot;
  *   GRAM  -- the dot is a lagged gather plus Gram corrections of the last 64
  *            steps, so the sequential chain does no memory access;
- *   AUTO  -- GRAM on sparse rows (mean nnz/row <= 512), CHAIN on long dense
- *            rows.  Takes effect at the next cocoa_init. */
+ *   DENSE -- dense rows (cocoa_set_train_dense, d even, d <= 4096): w and
+ *            deltaW in registers across a 512-thread workgroup, rows streamed;
+ *   AUTO  -- DENSE on dense rows that fit it, else GRAM on sparse rows (mean
+ *            nnz/row <= 512), else CHAIN.  Takes effect at the next cocoa_init. */
 #define COCOA_SOLVER_AUTO 0
 #define COCOA_SOLVER_CHAIN 1
 #define COCOA_SOLVER_GRAM 2
+#define COCOA_SOLVER_DENSE 3
 int cocoa_set_solver(cocoa_ctx *ctx, int kind);
 
 /* Start a run: alpha = 0 (CoCoA.scala:33), w = w_init (NULL = zeros,

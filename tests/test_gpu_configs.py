@@ -183,12 +183,12 @@ def c4():
 
 
 def test_c4_strict_bitwise_vs_oracle(c4):
-    """C4 with the double-buffered deltaW slices at their default (on: 128 x
-    3.23 M doubles = 3.3 GB per set)."""
+    """C4 with the deltaW layout at its default: compact slices (each partition's
+    distinct columns only, instead of 128 x 3.23 M dense doubles = 3.3 GB)."""
     sh, od, ot = c4
     e = make_engine(sh, strict=True)
     e.init("cocoa+", sh.n_glob, 2, sh.H, sh.lam)
-    assert e.plan()["dw_dbuf"] == 1
+    assert e.plan()["dw_compact"] == 1
     run = make_run(sh, od, "cocoa+")
     for t in (1, 2):
         e.round(t)
