@@ -38,7 +38,7 @@ $(DIAG)/libcocoa_hip.so: $(CSRC)/*.hip $(CSRC)/*.cpp $(HDRS)
 	mkdir -p $(DIAG)
 	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -ffp-contract=off -c $(CSRC)/kernels_strict.hip -o $(DIAG)/ks.o
 	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -DCOCOA_DIAG -ffp-contract=fast -munsafe-fp-atomics -c $(CSRC)/kernels_fast.hip -o $(DIAG)/kf.o
-	$(HIPCC) $(COMMON) -ffp-contract=off -c $(CSRC)/engine.hip -o $(DIAG)/en.o
+	$(HIPCC) $(COMMON) -DCOCOA_DIAG -ffp-contract=off -c $(CSRC)/engine.hip -o $(DIAG)/en.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DIAG)/ks.o $(DIAG)/kf.o $(DIAG)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o -lpthread -ldl
 
 oracle/liboracle.so: oracle/cocoa_oracle.c

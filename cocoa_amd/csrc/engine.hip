@@ -348,7 +348,12 @@ extern "C" int cocoa_create(int device, int strict, void* stream, cocoa_ctx** ou
         if (stream) {
             c->stream = (hipStream_t)stream;
         } else {
-            HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            // the round's own kernels (solver, fold, eval) at the highest priority:
+            // the side streams' work (next round's Gram rows, re-zeroing) yields
+            // dispatch slots to them
+            int lo = 0, hi = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
             c->own_stream = true;
         }
         HIPCHK(hipHostMalloc((void**)&c->h_eval, 8 * sizeof(double), hipHostMallocDefault));
@@ -628,7 +633,7 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
-    ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s);
+    ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s, eval_tile_entries());
     build_compact(ctx, row_ptr, pcol.data());
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
@@ -653,7 +658,7 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
     upload_col16(ctx->te.col16, pcol, nnz, ctx->d, s);
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
-    ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s);
+    ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s, eval_tile_entries());
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     if (ctx->inited) {
@@ -875,7 +880,9 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                 ctx->gt2.alloc(gtb);
                 ctx->samples2.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
                 if (!ctx->gstream) {
-                    HIPCHK(hipStreamCreateWithFlags(&ctx->gstream, hipStreamNonBlocking));
+                    int lo = 0, hi = 0;  // lowest priority: fills the CUs the solver leaves idle
+                    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                    HIPCHK(hipStreamCreateWithPriority(&ctx->gstream, hipStreamNonBlocking, lo));
                     HIPCHK(hipEventCreateWithFlags(&ctx->g_ready, hipEventDisableTiming));
                     for (auto& e : ctx->s_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
                 }

@@ -203,6 +203,7 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
                         hipStream_t s);
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
 int eval_fast_blocks(int64_t n, int64_t n_test);
+int eval_tile_entries();  // entries per fast-eval tile (make_tiles cap)
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 // Gram-window solver: lds bytes for a partition of max_nl rows (alpha in LDS
 // when it fits, else in alpha_work)

@@ -227,8 +227,20 @@ int eval_fast_blocks(int64_t n_tiles, int64_t n_t_tiles) {
     return (int)(b < 1 ? 1 : b);
 }
 
+int eval_tile_entries() {
+#ifdef COCOA_DIAG
+    // diagnostic builds only (make diag): A/B of the tile size
+    if (const char* e = getenv("COCOA_EVAL_TILE")) return atoi(e) == 2048 ? 2048 : kEvalTile;
+#endif
+    return kEvalTile;
+}
+
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
-    if (a.col16 && (a.n_test == 0 || a.t_col16))
+    const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
+    if (eval_tile_entries() == 2048) {
+        if (c16) eval_stream_kernel<2048, 512, true><<<blocks, 512, 0, s>>>(a);
+        else eval_stream_kernel<2048, 512, false><<<blocks, 512, 0, s>>>(a);
+    } else if (c16)
         eval_stream_kernel<kEvalTile, 512, true><<<blocks, 512, 0, s>>>(a);
     else
         eval_stream_kernel<kEvalTile, 512, false><<<blocks, 512, 0, s>>>(a);

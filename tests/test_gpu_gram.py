@@ -99,7 +99,7 @@ def test_gram_solver_repeated_rows_in_window(method):
     assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
 
 
-def test_gram_is_the_default_on_sparse_rows_and_chain_on_dense():
+def test_gram_is_the_default_on_sparse_rows_dense_on_dense_rows_chain_on_long_rows():
     sp = _small_parts()
     e = Engine(strict=False)
     e.set_train(sp)
@@ -117,6 +117,13 @@ def test_gram_is_the_default_on_sparse_rows_and_chain_on_dense():
     f = Engine(strict=False)
     f.set_train(dense)
     f.init("cocoa+", n, 1, 10, 1e-3)
-    assert f.plan()["solver"] == "chain"
+    assert f.plan()["solver"] == "dense"        # every row stores columns 0..d-1
+    # long rows that are not dense (1,200 of 5,000 columns): the chain solver
+    cols = np.concatenate([np.sort(rng.choice(5000, d, replace=False)) for _ in range(n)]).astype(np.int32)
+    longr = LabeledData(dense.row_ptr, cols, dense.val, dense.y, dense.part_ptr, 5000)
+    g = Engine(strict=False)
+    g.set_train(longr)
+    g.init("cocoa+", n, 1, 10, 1e-3)
+    assert g.plan()["solver"] == "chain"
     with pytest.raises(cocoa_amd.IllegalArgumentError):
         cocoa_amd._capi.check(cocoa_amd._capi.lib().cocoa_set_solver(f.h, 9), f.h)
