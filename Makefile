@@ -23,7 +23,7 @@ $(BUILD)/comm.o: $(CSRC)/comm.cpp $(HDRS) | $(BUILD)
 	$(HIPCC) -O2 -std=c++17 -fPIC -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -I$(CSRC) -x c++ -c $< -o $@
 
 OBJS := $(BUILD)/kernels_strict.strict.o $(BUILD)/kernels_fast.fast.o $(BUILD)/engine.strict.o $(BUILD)/dataset.o \
-        $(BUILD)/comm.o
+        $(BUILD)/comm.o $(BUILD)/ingest.strict.o
 
 $(OUT): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lpthread -ldl
@@ -39,7 +39,8 @@ $(DIAG)/libcocoa_hip.so: $(CSRC)/*.hip $(CSRC)/*.cpp $(HDRS)
 	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -ffp-contract=off -c $(CSRC)/kernels_strict.hip -o $(DIAG)/ks.o
 	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -DCOCOA_DIAG -ffp-contract=fast -munsafe-fp-atomics -c $(CSRC)/kernels_fast.hip -o $(DIAG)/kf.o
 	$(HIPCC) $(COMMON) -DCOCOA_DIAG -ffp-contract=off -c $(CSRC)/engine.hip -o $(DIAG)/en.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DIAG)/ks.o $(DIAG)/kf.o $(DIAG)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o -lpthread -ldl
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DIAG)/ks.o $(DIAG)/kf.o $(DIAG)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o \
+	    $(BUILD)/ingest.strict.o -lpthread -ldl
 
 oracle/liboracle.so: oracle/cocoa_oracle.c
 	$(MAKE) -s -C oracle

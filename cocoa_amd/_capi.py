@@ -121,6 +121,7 @@ SIGNATURES = {
     "cocoa_solver_profile_read": (_int, [_vp, ctypes.POINTER(ctypes.c_uint64), _i64]),
     "cocoa_sync": (_int, [_vp]),
     "cocoa_load_libsvm": (_int, [ctypes.c_char_p, _i32, _i32, ctypes.POINTER(Dataset)]),
+    "cocoa_load_libsvm_gpu": (_int, [_i32, ctypes.c_char_p, _i32, _i32, ctypes.POINTER(Dataset)]),
     "cocoa_gen_synthetic": (_int, [_i32, _i64, _i32, _f64, _i32, ctypes.c_uint64, _i64, _i32,
                                     ctypes.POINTER(Dataset)]),
     "cocoa_dataset_free": (None, [ctypes.POINTER(Dataset)]),

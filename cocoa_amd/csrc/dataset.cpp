@@ -22,6 +22,7 @@
 #include "common.h"
 #include "jdouble.h"
 #include "jrandom.h"
+#include "libsvm.h"
 
 namespace cocoa {
 
@@ -98,6 +99,8 @@ std::vector<int64_t> split_starts(int64_t size, int num_splits) {
 
 }  // namespace
 
+std::vector<int64_t> hadoop_split_starts(int64_t size, int num_splits) { return split_starts(size, num_splits); }
+
 }  // namespace cocoa
 
 using namespace cocoa;
@@ -110,6 +113,9 @@ static int host_fail(int code, const std::string& msg) {
     cocoa_set_global_error(msg);
     return code;
 }
+namespace cocoa {
+int host_error(int code, const std::string& msg) { return host_fail(code, msg); }
+}
 
 extern "C" void cocoa_dataset_free(cocoa_dataset* ds) {
     if (!ds) return;
@@ -121,7 +127,11 @@ extern "C" void cocoa_dataset_free(cocoa_dataset* ds) {
     std::memset(ds, 0, sizeof(*ds));
 }
 
-static bool ds_alloc(cocoa_dataset* ds, int64_t n, int64_t nnz, int32_t K) {
+namespace cocoa {
+bool dataset_alloc(cocoa_dataset* ds, int64_t n, int64_t nnz, int32_t K);
+}
+static bool ds_alloc(cocoa_dataset* ds, int64_t n, int64_t nnz, int32_t K) { return cocoa::dataset_alloc(ds, n, nnz, K); }
+bool cocoa::dataset_alloc(cocoa_dataset* ds, int64_t n, int64_t nnz, int32_t K) {
     ds->row_ptr = (int64_t*)std::malloc(sizeof(int64_t) * (size_t)(n + 1));
     ds->col = (int32_t*)std::malloc(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1));
     ds->val = (double*)std::malloc(sizeof(double) * (size_t)std::max<int64_t>(nnz, 1));
@@ -134,8 +144,8 @@ static bool ds_alloc(cocoa_dataset* ds, int64_t n, int64_t nnz, int32_t K) {
 // integer 1 -> +1, else -1), then "index:value" tokens split on single spaces,
 // index - 1 checked against numFeatures.  Writes y, the entries and their
 // count; on a malformed line returns the reference's exception kind.
-static int parse_line(const char* b, const char* le, int64_t r, int32_t num_features, double* y, int32_t* col,
-                      double* val, int64_t* z, std::string* msg) {
+int cocoa::libsvm_parse_line(const char* b, const char* le, int64_t r, int32_t num_features, double* y, int32_t* col,
+                             double* val, int64_t* z, std::string* msg) {
     int64_t k = 0;
     while (b < le && java_ws(*b)) ++b;  // line.trim()
     while (le > b && java_ws(le[-1])) --le;
@@ -268,7 +278,7 @@ extern "C" int cocoa_load_libsvm(const char* path, int32_t num_splits, int32_t n
             const int64_t p = line_beg[(size_t)r];
             const int64_t e = r + 1 < n ? line_beg[(size_t)r + 1] - 1 : S;
             std::string msg;
-            const int rc = parse_line(buf.data() + p, buf.data() + e, r, num_features, out->y + r,
+            const int rc = libsvm_parse_line(buf.data() + p, buf.data() + e, r, num_features, out->y + r,
                                       out->col + cap[(size_t)r], out->val + cap[(size_t)r], &zr[(size_t)r], &msg);
             if (rc != COCOA_OK) {
                 bad_line[(size_t)i] = r;
@@ -288,17 +298,10 @@ extern "C" int cocoa_load_libsvm(const char* path, int32_t num_splits, int32_t n
     // compaction of the slots (in place, moving left, only where a line had
     // fewer entries than ':' characters)
     int64_t nnz = 0;
-    int split = 0;
+    LinePartitioner lp(starts, K);
     out->row_ptr[0] = 0;
     for (int64_t r = 0; r < n; ++r) {
-        const int64_t p = line_beg[(size_t)r];
-        while (split + 1 < ns && p >= starts[(size_t)split + 1]) ++split;  // split holding the line's 1st byte
-        int part = split;
-        if (ns > K) {  // CoalescedRDD without locality: consecutive ranges of splits
-            part = 0;
-            while (part + 1 < K && (int64_t)split >= ((int64_t)(part + 1) * ns) / K) ++part;
-        }
-        out->part_ptr[part + 1]++;
+        out->part_ptr[lp.part(line_beg[(size_t)r]) + 1]++;
         const int64_t z = zr[(size_t)r], src = cap[(size_t)r];
         if (src != nnz && z > 0) {
             std::memmove(out->col + nnz, out->col + src, sizeof(int32_t) * (size_t)z);

@@ -69,10 +69,15 @@ def _from_c(ds):
     return out
 
 
-def load_libsvm(path, num_splits, num_features):
-    """OptUtils.loadLIBSVMData(sc, filename, numSplits, numFeats) (OptUtils.scala:11)."""
+def load_libsvm(path, num_splits, num_features, device=None):
+    """OptUtils.loadLIBSVMData(sc, filename, numSplits, numFeats) (OptUtils.scala:11).
+    device: a HIP device ordinal to tokenise and parse on (cocoa_load_libsvm_gpu);
+    None: the multithreaded host parse (cocoa_load_libsvm)."""
     ds = C.Dataset()
-    C.check(C.lib().cocoa_load_libsvm(path.encode(), num_splits, num_features, ctypes.byref(ds)))
+    if device is None:
+        C.check(C.lib().cocoa_load_libsvm(path.encode(), num_splits, num_features, ctypes.byref(ds)))
+    else:
+        C.check(C.lib().cocoa_load_libsvm_gpu(int(device), path.encode(), num_splits, num_features, ctypes.byref(ds)))
     return _from_c(ds)
 
 

@@ -287,6 +287,16 @@ typedef struct {
  * the file into num_splits partitions, label +1 iff the token contains '+'
  * or parses to 1, 1-based indices -> 0-based. */
 int cocoa_load_libsvm(const char *path, int32_t num_splits, int32_t num_features, cocoa_dataset *out);
+/* The same load with the tokenising and number parsing on HIP device `device`
+ * (the file is copied to HBM once; line starts, labels, "index:value" tokens
+ * and decimal values are found and converted by kernels, one wave per line).
+ * Lines outside the device's exact fast path (tabs or other characters inside
+ * a line, NaN/Infinity/hex spellings, more than 19 significant digits or a
+ * decimal exponent beyond +-22, malformed or out-of-range tokens) are parsed
+ * on the host by the same rules, so the dataset and the error raised are
+ * those of cocoa_load_libsvm. */
+int cocoa_load_libsvm_gpu(int device, const char *path, int32_t num_splits, int32_t num_features,
+                          cocoa_dataset *out);
 /* Seeded synthetic shapes: kind 0 = rcv1-like sparse
  * (Zipf columns, tf-idf-like values, unit rows), 1 = epsilon-like dense,
  * 2 = url-like very sparse binary-ish.  The rows are rows [first_row,
