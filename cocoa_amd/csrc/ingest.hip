@@ -1,7 +1,7 @@
 // GPU-side LIBSVM ingest: OptUtils.loadLIBSVMData (OptUtils.scala:11-53) with
 // the tokenising and number parsing on the device.
 //
-//   1. the file goes to HBM once (pinned staging, one copy);
+//   1. the file goes to HBM once;
 //   2. line starts: per 64 KB block a 256-thread workgroup counts newlines,
 //      the host scans the block counts, a second pass writes every line start
 //      in file order (block-local LDS scan);
@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -295,13 +296,15 @@ extern "C" int cocoa_load_libsvm_gpu(int device, const char* path, int32_t num_s
         std::fseek(f, 0, SEEK_END);
         const int64_t S = std::ftell(f);
         std::fseek(f, 0, SEEK_SET);
-        if (hipHostMalloc((void**)&hbuf, (size_t)S + 1, hipHostMallocDefault) != hipSuccess) {
+        // pageable buffer: pinning the whole file costs more than HIP's staged copy
+        hbuf = (char*)std::malloc((size_t)S + 1);
+        if (!hbuf) {
             std::fclose(f);
-            return host_error(COCOA_E_ARG, "cocoa_load_libsvm_gpu: out of pinned host memory");
+            return host_error(COCOA_E_ARG, "cocoa_load_libsvm_gpu: out of host memory");
         }
         if (S > 0 && std::fread(hbuf, 1, (size_t)S, f) != (size_t)S) {
             std::fclose(f);
-            (void)hipHostFree(hbuf);
+            std::free(hbuf);
             return host_error(COCOA_E_IO, std::string("read error on ") + path);
         }
         std::fclose(f);
@@ -369,7 +372,7 @@ extern "C" int cocoa_load_libsvm_gpu(int device, const char* path, int32_t num_s
                                              h.v.data(), &z, &msg);
             if (rc != COCOA_OK) {
                 (void)hipStreamDestroy(s);
-                (void)hipHostFree(hbuf);
+                std::free(hbuf);
                 return host_error(rc, msg);
             }
             h.c.resize((size_t)z);
@@ -414,11 +417,11 @@ extern "C" int cocoa_load_libsvm_gpu(int device, const char* path, int32_t num_s
             std::copy(h.v.begin(), h.v.end(), out->val + o);
         }
         (void)hipStreamDestroy(s);
-        (void)hipHostFree(hbuf);
+        std::free(hbuf);
         return COCOA_OK;
     } catch (const Error& e) {
         if (s) (void)hipStreamDestroy(s);
-        if (hbuf) (void)hipHostFree(hbuf);
+        if (hbuf) std::free(hbuf);
         cocoa_dataset_free(out);
         return host_error(e.code, e.what());
     }

@@ -61,7 +61,7 @@ constexpr int kGB = 16;                  // steps per batch
 constexpr int kGSlots = 64;              // window slots = lanes
 constexpr int kGNB = kGSlots / kGB;      // batches in the window
 constexpr int kGRing = 8;                // record / coefficient ring (batches)
-constexpr int kGHot = 64;                // dense hot columns of gram_kernel (device order: most frequent first)
+constexpr int kGHot = 32;                // dense hot columns of gram_kernel (device order: most frequent first)
 
 // ----------------------------------------------------------- LDS handoff --
 // The hand-offs order LDS data only (records, coefficients, layouts, staged
@@ -138,11 +138,11 @@ struct GramLds {
     int64_t pbeg[kGSlots];
     int32_t pcum[kGSlots + 1];       // packed offsets of the partners
 };
-static_assert(sizeof(GramLds) <= 80 * 1024, "gram_kernel LDS: two workgroups per CU");
+static_assert(sizeof(GramLds) * 3 <= 160 * 1024, "gram_kernel LDS: three workgroups per CU");
 
 __device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 21; }  // 11 bits
 
-__global__ __launch_bounds__(256, 2) void gram_kernel(GramArgs a) {
+__global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramLds& L = *(GramLds*)lds_raw;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
