@@ -51,7 +51,11 @@ class Comm:
 
 class Engine:
     def __init__(self, device=0, strict=False, stream=None):
-        """stream: a hipStream_t handle as int (e.g. torch.cuda.current_stream().cuda_stream)."""
+        """stream: a hipStream_t handle as int (e.g. torch.cuda.current_stream().cuda_stream).
+
+        A process that also uses torch on the GPU must initialise torch's HIP
+        runtime (torch ships its own libamdhip64) before the first Engine opens
+        the device, e.g. `import torch; torch.cuda.init()` first."""
         h = ctypes.c_void_p()
         C.check(C.lib().cocoa_create(int(device), 1 if strict else 0, ctypes.c_void_p(stream or 0), ctypes.byref(h)))
         self.h = h

@@ -9,6 +9,15 @@ if ROOT not in sys.path:
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# torch ships its own HIP/HSA runtime (torch/lib/libamdhip64.so); libcocoa_hip.so
+# links /opt/rocm's.  A process that uses both must bring torch's runtime up
+# first: once libcocoa_hip.so has opened the GPU, torch's copy finds no device.
+# The multi-rank tests hand device buffers to torch, so torch is loaded here.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and the built libcocoa_hip.so")
