@@ -190,18 +190,17 @@ def main():
     # tools/pmc_summary.py -> profiles/traffic.json), used only when the PMC run
     # profiled the same kernel variant this run launched
     plan = eng.plan()
-    solver_tag = "solver_kernel<"
-    eval_tag = "eval_stream_kernel<"
+    # HBM traffic per launch from the committed PMC passes, only for the kernels
+    # this run launched (fast mode, the C2 headline workload the passes profiled)
     traffic = traffic_eval = None
     tf = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tf) and not args.strict:
+    if os.path.exists(tf) and not args.strict and args.config == "c2" and args.method == "cocoa+" and world == 1:
         try:
             tk = json.load(open(tf)).get("kernels", {})
-            for rec in tk.values():
-                if solver_tag in rec["kernel"] and "<0, false" in rec["kernel"].replace("cocoa::", ""):
-                    traffic = rec["hbm_bytes_per_launch"]
-                if eval_tag in rec["kernel"]:
-                    traffic_eval = rec["hbm_bytes_per_launch"]
+            rec = tk.get("solver_" + plan.get("solver", ""))
+            traffic = rec["hbm_bytes_per_launch"] if rec else None
+            rec = tk.get("eval")
+            traffic_eval = rec["hbm_bytes_per_launch"] if rec else None
         except Exception:
             traffic = traffic_eval = None
     eval_ms = stats["eval"]["total_ms"] / max(stats["eval"]["launches"], 1)

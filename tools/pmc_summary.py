@@ -44,9 +44,14 @@ def main():
            "calibration": {"fetch_bytes_per_reported_byte_f64": k_f64, "fetch_bytes_per_reported_byte_i32": k_i32,
                            "write_bytes_per_reported_byte_f64": k_w},
            "kernels": {}}
-    for tag, needle in (("solver", "solver_kernel"), ("solver2", "solver2_kernel"), ("eval", "eval"),
-                        ("plan", "plan_kernel"), ("fold", "fold_kernel"), ("apply", "apply_kernel")):
-        names = sorted({k for (k, c) in f if needle in k and "final" not in k})
+    # tag -> (substring the kernel name must hold, substrings it must not hold)
+    tags = (("solver_chain", "solver_kernel<", ()), ("solver_gram", "solver_gram_kernel", ()),
+            ("solver_dense", "dense_solver_kernel", ()), ("gram", "gram_kernel", ("solver_gram",)),
+            ("eval", "eval_stream_kernel", ()), ("eval_dense", "eval_dense_kernel", ()),
+            ("plan", "plan_kernel", ()), ("fold", "fold_kernel", ("compact",)),
+            ("fold_compact", "fold_compact_kernel", ()), ("apply", "apply_kernel", ()))
+    for tag, needle, bad in tags:
+        names = sorted({k for (k, c) in f if needle in k and not any(b in k for b in bad)})
         if not names:
             continue
         fe, n = pick(f, names[0], "FETCH_SIZE")
