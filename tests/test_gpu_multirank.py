@@ -157,3 +157,81 @@ def test_multirank_fast_allreduce_within_tolerance():
         for ev, rv in zip(out[0][m][2], revs):
             assert abs(ev["primal"] - rv["primal"]) <= 1e-9 * abs(rv["primal"])
             assert ev["test_err_count"] == rv["test_err"]
+
+
+# ---- dense rows (dense solver) and compact deltaW slices across ranks ----
+def _cfg_worker(rank, world, strict, cfg, uid_q, out_q):
+    try:
+        from cocoa_amd import configs
+        if cfg.get("compact"):
+            os.environ["COCOA_DW_COMPACT"] = "1"
+        sh = configs.share(cfg["config"], rank=rank, world=world, scaling="strong", n=cfg["n"], d=cfg.get("d"),
+                           parts=cfg["parts"], n_test=cfg["n_test"])
+        if rank == 0:
+            uid = comm_unique_id("host")
+            for _ in range(world - 1):
+                uid_q.put(uid)
+        else:
+            uid = uid_q.get(timeout=60)
+        e = Engine(device=0, strict=strict)
+        e.set_train(sh.train, part_begin=sh.part_begin, num_parts_global=sh.k_glob)
+        e.set_test(sh.test)
+        e.comm_init("host", rank, world, uid)
+        e.init("cocoa+", sh.n_glob, 4, sh.H, sh.lam)
+        plan = e.plan()
+        for t in range(1, 5):
+            e.round(t)
+        out_q.put((rank, (e.w(), e.alpha(), e.eval(), plan)))
+        e.close()
+    except Exception as ex:
+        out_q.put((rank, repr(ex)))
+
+
+@pytest.mark.parametrize("cfg,strict", [
+    (dict(config="c3", n=4096, parts=8, n_test=256), False),
+    (dict(config="c4", n=16000, d=200000, parts=8, n_test=400, compact=True), False),
+    (dict(config="c4", n=16000, d=200000, parts=8, n_test=400, compact=True), True),
+])
+def test_multirank_dense_and_compact_layouts(cfg, strict):
+    from cocoa_amd import configs
+    world = 2
+    ctx = mp.get_context("spawn")
+    uid_q, out_q = ctx.Queue(), ctx.Queue()
+    procs = [ctx.Process(target=_cfg_worker, args=(r, world, strict, cfg, uid_q, out_q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = dict(out_q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert not isinstance(out[r], str), out[r]
+    want = "dense" if cfg["config"] == "c3" and not strict else ("gram" if not strict else "chain")
+    assert out[0][3]["solver"] == want
+    if cfg.get("compact"):
+        assert out[0][3]["dw_compact"] == 1
+    sh = configs.share(cfg["config"], n=cfg["n"], d=cfg.get("d"), parts=cfg["parts"], n_test=cfg["n_test"],
+                       scaling="strong")
+    od = oracle.Data(sh.train.row_ptr, sh.train.col, sh.train.val, sh.train.y, sh.train.part_ptr,
+                     sh.train.num_features)
+    ot = oracle.Data(sh.test.row_ptr, sh.test.col, sh.test.val, sh.test.y, sh.test.part_ptr, sh.test.num_features)
+    run = oracle.Run(od, "cocoa+", sh.n_glob, sh.H, sh.lam, nthreads=16)
+    for t in range(1, 5):
+        run.round(t)
+    rv = run.eval(ot)
+    w_ref = run.w()
+    a = np.concatenate([out[r][1] for r in range(world)])
+    ev = out[0][2]
+    assert out[0][0].tobytes() == out[1][0].tobytes()  # w identical on every rank
+    if strict:
+        assert out[0][0].tobytes() == w_ref.tobytes()
+        assert a.tobytes() == run.alpha().tobytes()
+        assert ev["gap"].hex() == rv["gap"].hex()
+    else:
+        assert np.max(np.abs(out[0][0] - w_ref)) <= 1e-9 * np.max(np.abs(w_ref))
+        assert np.max(np.abs(a - run.alpha())) <= 1e-9
+        assert abs(ev["gap"] - rv["gap"]) <= 1e-9 * abs(rv["primal"])
+    assert ev["test_err_count"] == rv["test_err"]
