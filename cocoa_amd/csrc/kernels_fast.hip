@@ -248,8 +248,8 @@ void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
 }
 
 // ------------------------------------------------------------ dense rows --
-// 16-byte column chunks per thread: CPT * 512 * 2 >= d
-static int dense_cpt(int64_t d) { return d <= 1024 ? 1 : d <= 2048 ? 2 : d <= 4096 ? 4 : 0; }
+// 16-byte column chunks per thread: CPT * kDT * 2 >= d
+static int dense_cpt(int64_t d) { return d <= 512 ? 1 : d <= 1024 ? 2 : d <= 2048 ? 4 : d <= 4096 ? 8 : 0; }
 
 bool dense_solver_fits(int64_t d, int64_t max_nl) {
     return d >= 2 && (d & 1) == 0 && dense_cpt(d) > 0 && max_nl >= 1 && max_nl * 8 <= 150 * 1024;
@@ -258,18 +258,20 @@ bool dense_eval_fits(int64_t d) { return d >= 2 && (d & 1) == 0 && d <= 4096; }
 
 template <int MODE, int CPT, int P>
 static void launch_ds(const DenseArgs& a, int grid, size_t lds, hipStream_t s) {
-    (void)hipFuncSetAttribute((const void*)dense_solver_kernel<MODE, CPT, P>,
+    (void)hipFuncSetAttribute((const void*)dense_solver_kernel<MODE, CPT, P, kDT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dense_solver_kernel<MODE, CPT, P><<<grid, kDT, lds, s>>>(a);
+    dense_solver_kernel<MODE, CPT, P, kDT><<<grid, kDT, lds, s>>>(a);
 }
 
 template <int MODE>
 static void launch_ds_mode(const DenseArgs& a, int grid, size_t lds, hipStream_t s) {
-    // P = rows in flight per workgroup: 16 KB each at d = 2,000
+    // P = rows in flight per workgroup (16 KB each at d = 2,000); the ring is
+    // P * CPT * 4 VGPRs
     switch (dense_cpt(a.d)) {
         case 1: launch_ds<MODE, 1, 16>(a, grid, lds, s); break;
-        case 2: launch_ds<MODE, 2, 8>(a, grid, lds, s); break;
-        default: launch_ds<MODE, 4, 4>(a, grid, lds, s); break;
+        case 2: launch_ds<MODE, 2, 16>(a, grid, lds, s); break;
+        case 4: launch_ds<MODE, 4, 8>(a, grid, lds, s); break;
+        default: launch_ds<MODE, 8, 4>(a, grid, lds, s); break;
     }
 }
 

@@ -4,14 +4,14 @@
 // column indices at all.
 //
 // dense_solver_kernel -- CoCoA.localSDCA (CoCoA.scala:148-188) and the MbCD
-// local solver (MinibatchCD.scala:95-125), one 512-thread workgroup per
+// local solver (MinibatchCD.scala:95-125), one 256-thread workgroup per
 // partition.  deltaW and w never touch memory during the round: thread t owns
-// the 16-byte column chunks t, t + 512, ... of the row and keeps w and deltaW
+// the 16-byte column chunks t, t + 256, ... of the row and keeps w and deltaW
 // for those columns in registers.  Per step:
 //   1. the thread's partial of x.w (+ sigma x.deltaW for CoCoA+, + x.deltaW
 //      for CoCoA, whose task-local w is w + deltaW) over its chunks (FMA);
 //   2. a DPP wave sum, one LDS slot per wave, ONE workgroup barrier, and every
-//      thread adds the 8 wave sums in the same order (so every thread holds the
+//      thread adds the 4 wave sums in the same order (so every thread holds the
 //      same dot and evaluates the same update rule: no broadcast round trip);
 //   3. deltaW += c x on the thread's chunks, in registers; lane 0 of every
 //      wave stores the new alpha (alpha of the partition lives in LDS; each
@@ -32,29 +32,35 @@ namespace cocoa {
 
 typedef double f64x2v __attribute__((ext_vector_type(2)));
 
-constexpr int kDT = 512;       // dense solver threads (8 waves)
-constexpr int kDWv = kDT / 64;
+// threads of a dense-solver workgroup: one wave per SIMD.  The chain is issue
+// bound -- every wave runs the whole per-step sequence (DPP reduction, update
+// rule, address arithmetic, ~100 instructions around its FMAs), so two waves
+// per SIMD (512 threads) took twice the cycles per step of one (C3: 2.70 ms
+// per round with 512 threads)
+constexpr int kDT = 256;
 
 __device__ __forceinline__ f64x2v ld_nt2(const double* p) { return __builtin_nontemporal_load((const f64x2v*)p); }
 
-template <int MODE, int CPT, int P>
-__global__ __launch_bounds__(kDT) void dense_solver_kernel(DenseArgs a) {
+
+template <int MODE, int CPT, int P, int NTH>
+__global__ __launch_bounds__(NTH) void dense_solver_kernel(DenseArgs a) {
+    constexpr int NWV = NTH / 64;
     extern __shared__ double al[];  // alpha of the partition (rows [p0, p0 + nl))
-    __shared__ double red[2][kDWv];
+    __shared__ double red[2][NWV];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int k = blockIdx.x;
     const int64_t p0 = a.part_ptr[k];
     const int32_t nl = (int32_t)(a.part_ptr[k + 1] - p0);
     const int32_t H = a.H;
     const int64_t d = a.d, nch = d >> 1;
-    for (int i = tid; i < nl; i += kDT) al[i] = a.alpha[p0 + i];
+    for (int i = tid; i < nl; i += NTH) al[i] = a.alpha[p0 + i];
 
     int64_t cof[CPT];
     bool okc[CPT];
     f64x2v wr[CPT], dr[CPT];
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-        const int64_t ci = tid + (int64_t)kDT * c;
+        const int64_t ci = tid + (int64_t)NTH * c;
         const bool ok = ci < nch;
         okc[c] = ok;
         cof[c] = 2 * (ok ? ci : nch - 1);  // past the row: an in-row address, w = deltaW = 0 (kept 0)
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(kDT) void dense_solver_kernel(DenseArgs a) {
                 __syncthreads();
                 double tot = red[s & 1][0];
 #pragma unroll
-                for (int i = 1; i < kDWv; ++i) tot += red[s & 1][i];
+                for (int i = 1; i < NWV; ++i) tot += red[s & 1][i];
                 const double yv = readlane_d(y0, j), rq = readlane_d(rq0, j);
                 const double grad = (yv * tot - 1.0) * a.lam_n;  // CoCoA.scala:157-163
                 // projection + skip (CoCoA.scala:166-172) fold into the clamp: a
@@ -146,12 +152,12 @@ __global__ __launch_bounds__(kDT) void dense_solver_kernel(DenseArgs a) {
     double* dk = a.dw + (size_t)k * (size_t)d;
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-        const int64_t ci = tid + (int64_t)kDT * c;
+        const int64_t ci = tid + (int64_t)NTH * c;
         if (ci < nch) *(f64x2v*)(dk + 2 * ci) = dr[c];
     }
     __syncthreads();
     // alpha <- alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101)
-    for (int i = tid; i < nl; i += kDT) {
+    for (int i = tid; i < nl; i += NTH) {
         const double old = a.alpha[p0 + i];
         a.alpha[p0 + i] = old + (al[i] - old) * a.scaling;
     }
