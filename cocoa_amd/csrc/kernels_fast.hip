@@ -41,11 +41,22 @@ void launch_gram(const GramArgs& a, hipStream_t s) {
     if (grid > 0) gram_kernel<<<(unsigned)grid, 256, sizeof(GramLds), s>>>(a);
 }
 
-template <int MODE>
+template <int MODE, bool HOTLDS>
 static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
-    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    solver_gram_kernel<MODE><<<grid, kGThreads, lds, s>>>(a);
+    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    solver_gram_kernel<MODE, HOTLDS><<<grid, kGThreads, lds, s>>>(a);
+}
+
+// deltaW columns in LDS (HOTLDS) or all in the L2-resident slice.  The memory
+// wave is VALU-issue bound, and the LDS path costs it a select and an LDS read
+// per gathered entry: without it the C2 solver measured 9% faster (r02,
+// tools/gpu_r02w.sh), so the LDS path is only in the diagnostic build.
+static bool gram_hot_lds() {
+#ifdef COCOA_DIAG
+    if (const char* e = getenv("COCOA_GRAM_HOTLDS")) return atoi(e) != 0;  // diagnostic A/B only
+#endif
+    return false;
 }
 
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s) {
@@ -60,9 +71,17 @@ void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t
     }
     if (const char* e = getenv("COCOA_GRAM_DIAG")) g.diag = atoi(e);
 #endif
-    if (mode == MODE_PLUS) launch_sg<MODE_PLUS>(g, grid, lds, s);
-    else if (mode == MODE_COCOA) launch_sg<MODE_COCOA>(g, grid, lds, s);
-    else launch_sg<MODE_MBCD>(g, grid, lds, s);
+    if (!gram_hot_lds()) {
+        lds -= sizeof(double) * (size_t)g.hot;
+        g.hot = 0;
+        if (mode == MODE_PLUS) launch_sg<MODE_PLUS, false>(g, grid, lds, s);
+        else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, false>(g, grid, lds, s);
+        else launch_sg<MODE_MBCD, false>(g, grid, lds, s);
+        return;
+    }
+    if (mode == MODE_PLUS) launch_sg<MODE_PLUS, true>(g, grid, lds, s);
+    else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, true>(g, grid, lds, s);
+    else launch_sg<MODE_MBCD, true>(g, grid, lds, s);
 }
 
 // ----------------------------------------------------------- fused eval --

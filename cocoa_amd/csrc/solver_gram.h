@@ -418,13 +418,13 @@ __device__ __forceinline__ double ring_val(const GramSolverLds& S, int32_t ri) {
 //                          marks) and row layouts, up to kGRing batches ahead;
 //   waves 3..    fetch  -- copy each batch's (column, value) entries into the
 //                          LDS ring (LDS DMA), ahead of the gathers.
-template <int MODE>
+template <int MODE, bool HOTLDS>
 __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramSolverLds& S = *(GramSolverLds*)lds_raw;
     // LDS after the hand-off state: deltaW of the hot columns [0, a.hot)
     double* hotl = (double*)(lds_raw + ((sizeof(GramSolverLds) + 15) & ~(size_t)15));
-    const int32_t hot = a.hot;
+    const int32_t hot = HOTLDS ? a.hot : 0;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int k = blockIdx.x;
     const int32_t H = a.H, NB = (H + kGB - 1) / kGB;
@@ -584,10 +584,10 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         uint32_t hrow[(kGMaxU + 5) / 6];  //   and their rows (5 bits per unit, 31 = no entry)
         int32_t xin = -1;               // batch whose gathers are in flight
         auto dw_add = [&](int32_t c, double v) {
-            if (c < hot) __hip_atomic_fetch_add(hotl + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (HOTLDS && c < hot) __hip_atomic_fetch_add(hotl + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             else unsafeAtomicAdd(dwk + c, v);
         };
-        auto dw_get = [&](int32_t c) { return c < hot ? hotl[c] : dw_load(dwk + c); };
+        auto dw_get = [&](int32_t c) { return (HOTLDS && c < hot) ? hotl[c] : dw_load(dwk + c); };
         auto fetched = [&](int32_t x) {
             return wait_ge(&S.cnt[kCFetch + x % kGFetch], x + 1, abortf, a.status, pw);
         };
@@ -721,15 +721,22 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                                 const int32_t c = rw[t] < kGB ? cl[t] : -1;
                                 // a hot (LDS) or empty lane loads the constant 1 -- one register
                                 // never mixes a global load with an LDS read (that would serialise)
-                                if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(c >= hot ? dwk + c : &g_gram_one);
-                                hx[t] = hotl[(c >= 0 && c < hot) ? c : 0];
+                                if (HOTLDS) {
+                                    if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(c >= hot ? dwk + c : &g_gram_one);
+                                    hx[t] = hotl[(c >= 0 && c < hot) ? c : 0];
+                                } else if (!(COCOA_DIAG_ON && (a.diag & 2))) {
+                                    dw[u] = dw_load(c >= 0 ? dwk + c : &g_gram_one);
+                                }
                             }
                             __builtin_amdgcn_sched_barrier(0);  // all reads of the group out before the products
 #pragma unroll
                             for (int t = 0; t < 8; ++t) {
                                 const int u = u0 + t;
                                 const bool ok = rw[t] < kGB;
-                                hv[u] = ok ? ((cl[t] < hot) ? vl[t] * hx[t] : vl[t]) : 0.0;
+                                if (HOTLDS)
+                                    hv[u] = ok ? ((cl[t] < hot) ? vl[t] * hx[t] : vl[t]) : 0.0;
+                                else
+                                    hv[u] = ok ? vl[t] : 0.0;
                                 hrow[u / 6] = (hrow[u / 6] & ~(31u << (5 * (u % 6)))) | ((uint32_t)(ok ? rw[t] : 31) << (5 * (u % 6)));
                             }
                         }
