@@ -364,7 +364,7 @@ struct GramSolverLds {
     double coef[kGRing * kGB];         // c_j, same ring (chain -> memory wave)
     GLay lay[kGRing];                  // same ring (loader -> fetch / memory waves)
     double base[kGSlots];              // base_s per slot (memory wave -> chain)
-    double part[kGB][64];              // memory wave: per-lane row partial sums of a batch's products
+    double part[kGB + 1][64];          // memory wave: per-lane row partial sums of a batch's products (+ a sink row)
     double gring[kGGt][kGB][kGSlots];  // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
     int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
     int32_t ecol[kGE];                 // staged entries (fetch waves -> memory wave): column,
@@ -583,6 +583,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         double hv[kGMaxU], dw[kGMaxU];  // in-flight gathers: staged value (x hot deltaW), loaded deltaW (or 1)
         uint32_t hrow[(kGMaxU + 5) / 6];  //   and their rows (5 bits per unit, 31 = no entry)
         int32_t xin = -1;               // batch whose gathers are in flight
+        int32_t xnu = 0;                //   and its 64-entry units
         auto dw_add = [&](int32_t c, double v) {
             if (HOTLDS && c < hot) __hip_atomic_fetch_add(hotl + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             else unsafeAtomicAdd(dwk + c, v);
@@ -613,19 +614,17 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             if (xin >= 0) {
 #pragma unroll
                 for (int i = 0; i < kGB; ++i) S.part[i][lane] = 0.0;
-                int cur = -1;
-                double run = 0.0;
+                // every unit adds its product into (its row, this lane): a fire-and-forget
+                // LDS add per unit, no branch (entries past the batch go to the sink row);
+                // the units past the batch are skipped as a whole (uniform branch)
 #pragma unroll
                 for (int u = 0; u < kGMaxU; ++u) {
-                    const int row = (int)((hrow[u / 6] >> (5 * (u % 6))) & 31u);  // 31: no entry
-                    if (row != cur) {
-                        if (cur >= 0 && cur < kGB) S.part[cur][lane] = run;
-                        cur = row;
-                        run = 0.0;
+                    if (u < xnu) {
+                        const int row = min((int)((hrow[u / 6] >> (5 * (u % 6))) & 31u), kGB);  // 31: no entry
+                        __hip_atomic_fetch_add(&S.part[row][lane], hv[u] * dw[u], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    run = fma(hv[u], dw[u], run);
                 }
-                if (cur >= 0 && cur < kGB) S.part[cur][lane] = run;
                 wave_lds_sync();
                 const int rr = lane >> 2, qq = (lane & 3) * 16;
                 double s4 = 0.0;
@@ -695,12 +694,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 if (pos >= 0) {
                     if (!fetched(x)) break;
 #pragma unroll
-                    for (int w = 0; w < (kGMaxU + 5) / 6; ++w) hrow[w] = 0xFFFFFFFFu;
-#pragma unroll
-                    for (int u = 0; u < kGMaxU; ++u) {
-                        hv[u] = 0.0;
-                        dw[u] = 1.0;
-                    }
+                    for (int w = 0; w < (kGMaxU + 5) / 6; ++w) hrow[w] = 0xFFFFFFFFu;  // units past nu: never read
 #pragma unroll
                     for (int u0 = 0; u0 < kGMaxU; u0 += 8) {
                         if (u0 < nu) {
@@ -742,6 +736,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         }
                     }
                     xin = x;
+                    xnu = nu;
                 } else {
                     // too long to stage: gathered and summed here
                     double* bs = S.base + (x % kGNB) * kGB;
