@@ -38,7 +38,7 @@ void launch_gram(const GramArgs& a, hipStream_t s) {
         attr = true;
     }
     const int64_t grid = (int64_t)a.K * a.nbatch;
-    if (grid > 0) gram_kernel<<<(unsigned)grid, 256, sizeof(GramLds), s>>>(a);
+    if (grid > 0) gram_kernel<<<(unsigned)grid, kGramThreads, sizeof(GramLds), s>>>(a);
 }
 
 template <int MODE, bool HOTLDS>

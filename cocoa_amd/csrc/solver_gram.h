@@ -123,8 +123,9 @@ __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F
 // Windows longer than the register chunk reload it per tile (same results).
 constexpr int kGramTable = 2048;     // hash slots (power of two, 2 x kGramTile)
 constexpr int kGramTile = 1024;      // updater positions per hash tile
-constexpr int kGramNU = 24;          // 256-entry units in registers
-constexpr int kGramCH = kGramNU * 256;
+constexpr int kGramThreads = 512;    // 8 waves: two workgroups (53 KB of LDS each) give 16 waves per CU
+constexpr int kGramNU = 12;          // kGramThreads-entry units in registers
+constexpr int kGramCH = kGramNU * kGramThreads;
 constexpr int kGHotS = kGHot + 1;    // XP row stride (doubles)
 
 struct GramLds {
@@ -138,11 +139,12 @@ struct GramLds {
     int64_t pbeg[kGSlots];
     int32_t pcum[kGSlots + 1];       // packed offsets of the partners
 };
-static_assert(sizeof(GramLds) * 3 <= 160 * 1024, "gram_kernel LDS: three workgroups per CU");
+static_assert(sizeof(GramLds) * 2 <= 160 * 1024, "gram_kernel LDS: two workgroups per CU");
+static_assert(kGramThreads == 512, "gram_kernel's hot part gives each of the 8 waves two updaters");
 
 __device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 21; }  // 11 bits
 
-__global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
+__global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramLds& L = *(GramLds*)lds_raw;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -188,8 +190,8 @@ __global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
         L.pcum[lane + 1] = inc;
         if (lane == 0) L.pcum[0] = 0;
     }
-    for (int i = tid; i < kGSlots * kGHotS; i += 256) (&L.XP[0][0])[i] = 0.0;
-    for (int i = tid; i < kGB * kGSlots; i += 256) (&L.acc[0][0])[i] = 0.0;
+    for (int i = tid; i < kGSlots * kGHotS; i += kGramThreads) (&L.XP[0][0])[i] = 0.0;
+    for (int i = tid; i < kGB * kGSlots; i += kGramThreads) (&L.acc[0][0])[i] = 0.0;
     __syncthreads();
     phase(0);
     const int32_t T = L.pcum[P], Q16 = L.pcum[U];
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
         int o[kGramNU];
 #pragma unroll
         for (int u = 0; u < kGramNU; ++u) {  // owners: independent binary searches, interleaved
-            const int32_t q = min(qa + u * 256 + tid, T - 1);
+            const int32_t q = min(qa + u * kGramThreads + tid, T - 1);
             int lo = 0;
 #pragma unroll
             for (int st = kGSlots / 2; st >= 1; st >>= 1)
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < kGramNU; ++u) {
-            const int32_t q = qa + u * 256 + tid;
+            const int32_t q = qa + u * kGramThreads + tid;
             const bool ok = q < T;
             const int64_t e = ok ? L.pbeg[o[u]] + (q - L.pcum[o[u]]) : 0;
             cc[u] = ok ? a.col[e] : -1;
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
     phase(1);
     // cold part, one hash tile of updater positions at a time
     for (int32_t ta = 0; ta < Q16; ta += kGramTile) {
-        for (int i = tid; i < kGramTable; i += 256) {
+        for (int i = tid; i < kGramTable; i += kGramThreads) {
             L.tkey[i] = -1;
             L.thead[i] = -1;
         }
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
             load(qa);
 #pragma unroll
             for (int u = 0; u < kGramNU; ++u) {
-                const int32_t q = qa + u * 256 + tid;
+                const int32_t q = qa + u * kGramThreads + tid;
                 const int32_t c = cc[u];
                 if (q >= ta && q < tb && c >= kGHot) {
                     const int32_t i = q - ta;
@@ -292,28 +294,24 @@ __global__ __launch_bounds__(256, 3) void gram_kernel(GramArgs a) {
         phase(6);
     }
     phase(2);
-    // hot part: wave wv -> updaters 4 wv .. 4 wv + 3, lane = partner
+    // hot part: wave wv -> updaters 2 wv, 2 wv + 1, lane = partner
     {
-        double h0 = 0.0, h1 = 0.0, h2 = 0.0, h3 = 0.0;
-        const int u0 = 4 * wv;
+        double h0 = 0.0, h1 = 0.0;
+        const int u0 = 2 * wv;
 #pragma unroll 8
         for (int c = 0; c < kGHot; ++c) {
             const double xp = L.XP[lane][c];
             h0 = fma(L.XP[u0][c], xp, h0);
             h1 = fma(L.XP[u0 + 1][c], xp, h1);
-            h2 = fma(L.XP[u0 + 2][c], xp, h2);
-            h3 = fma(L.XP[u0 + 3][c], xp, h3);
         }
         L.acc[u0][lane] += h0;  // sole writer of (u, lane) now
         L.acc[u0 + 1][lane] += h1;
-        L.acc[u0 + 2][lane] += h2;
-        L.acc[u0 + 3][lane] += h3;
     }
     __syncthreads();
     phase(3);
     // Gt rows of the block's updaters: slot of partner p = (j0 + p) & 63
     double* out = a.gt + ((size_t)k * a.nbatch * kGB + j0) * kGSlots;
-    for (int u = wv; u < kGB; u += 4) {
+    for (int u = wv; u < kGB; u += kGramThreads / 64) {
         const double v = (u < U && lane > u && lane < P) ? L.acc[u][lane] : 0.0;
         __builtin_nontemporal_store(v, out + (size_t)u * kGSlots + ((j0 + lane) & (kGSlots - 1)));
     }
