@@ -717,7 +717,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                                     if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(c >= hot ? dwk + c : &g_gram_one);
                                     hx[t] = hotl[(c >= 0 && c < hot) ? c : 0];
                                 } else if (!(COCOA_DIAG_ON && (a.diag & 2))) {
-                                    dw[u] = dw_load(c >= 0 ? dwk + c : &g_gram_one);
+                                    // a lane past the batch loads column 0: its product goes to the sink row
+                                    dw[u] = dw_load(dwk + (c >= 0 ? c : 0));
                                 }
                             }
                             __builtin_amdgcn_sched_barrier(0);  // all reads of the group out before the products
@@ -728,7 +729,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                                 if (HOTLDS)
                                     hv[u] = ok ? ((cl[t] < hot) ? vl[t] * hx[t] : vl[t]) : 0.0;
                                 else
-                                    hv[u] = ok ? vl[t] : 0.0;
+                                    hv[u] = vl[t];  // past the batch: any value, summed into the sink row
                                 hrow[u / 6] = (hrow[u / 6] & ~(31u << (5 * (u % 6)))) | ((uint32_t)(ok ? rw[t] : 31) << (5 * (u % 6)));
                             }
                         }
