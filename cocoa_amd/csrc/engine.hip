@@ -984,7 +984,9 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         // (samples, Gram rows) of this round: prefetched during the last round's
         // solver (overlap), else computed here
         const bool gram_rows = c->use_gram && c->method != COCOA_METHOD_MBCD;
-        const bool overlap = gram_rows && c->gstream && c->gt2.p;
+        // COCOA_GRAM_SERIAL=1 (diagnostic A/B only): Gram rows in line, before the solver
+        static const bool serial = std::getenv("COCOA_GRAM_SERIAL") && std::atoi(std::getenv("COCOA_GRAM_SERIAL"));
+        const bool overlap = gram_rows && c->gstream && c->gt2.p && !serial;
         int b = 0;
         if (overlap && c->pre_t == t) {
             b = c->pre_buf;

@@ -359,7 +359,7 @@ constexpr int kCChain = 0, kCScat = 1, kCBase = 2, kCLoad = 3, kCAbort = 4, kCFr
 struct GramSolverLds {
     int cnt[16];
     GRec rec[kGRing * kGB];            // ring: (b % kGRing) * kGB + i
-    double coef[kGRing * kGB];         // c_j, same ring (chain -> memory wave)
+    double coef[kGRing * 2 * kGB];     // c_j, same ring (chain -> memory wave); [kGB, 2 kGB) of a slot stay 0
     GLay lay[kGRing];                  // same ring (loader -> fetch / memory waves)
     double base[kGSlots];              // base_s per slot (memory wave -> chain)
     double part[kGB + 1][64];          // memory wave: per-lane row partial sums of a batch's products (+ a sink row)
@@ -403,6 +403,12 @@ __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
     __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
 
+// 0 for a unit of the batch (u < nu), 0xFF (row: no entry) past it.  The row byte is
+// read unconditionally and or-ed with this: a branch around the read would make
+// every unit wait for its LDS read before the next one goes out.
+__device__ __forceinline__ uint32_t gram_pad(int32_t u, int32_t nu) {
+    return (uint32_t)((nu - 1 - u) >> 31) & 0xFFu;
+}
 __device__ __forceinline__ double ring_val(const GramSolverLds& S, int32_t ri) {
     return __hiloint2double((int)S.evhi[ri], (int)S.evlo[ri]);
 }
@@ -439,6 +445,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     if (tid == 0) alv[nl] = 0.0;
     for (int i = tid; i < kGSlots; i += kGThreads) S.base[i] = 0.0;  // batches 0 .. kGNB-1: deltaW is still zero
     for (int32_t i = tid; i < hot; i += kGThreads) hotl[i] = 0.0;
+    for (int i = tid; i < kGRing * 2 * kGB; i += kGThreads) S.coef[i] = 0.0;  // zero slots: rows past a batch
     if (tid < 16) S.cnt[tid] = 0;
     __syncthreads();
     if (tid == 0) S.cnt[kCBase] = kGNB;
@@ -639,7 +646,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             // 2. deltaW += c_j x_j for the steps of batch b (CoCoA.scala:181-185)
             {
                 const GLay& L = S.lay[b % kGRing];
-                const double* cf = S.coef + (b % kGRing) * kGB;
+                const double* cf = S.coef + (b % kGRing) * (2 * kGB);
                 const int32_t pos = L.pos, nu = L.nu;
                 if (pos >= 0) {
                     if (!fetched(b)) break;
@@ -654,12 +661,12 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 #pragma unroll
                         for (int t = 0; t < 8; ++t) {
                             const int32_t ri = ((pos + (u0 + t) * 64) & (kGE - 1)) + lane;
-                            rw[t] = u0 + t < nu ? S.erow[ri] : 0xFF;
+                            rw[t] = S.erow[ri] | gram_pad(u0 + t, nu);
                             cl[t] = S.ecol[ri];
                             vl[t] = ring_val(S, ri);
                         }
 #pragma unroll
-                        for (int t = 0; t < 8; ++t) cc[t] = rw[t] < kGB ? cf[rw[t] & (kGB - 1)] : 0.0;
+                        for (int t = 0; t < 8; ++t) cc[t] = cf[rw[t] & (2 * kGB - 1)];  // row 0xFF: a zero slot
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int t = 0; t < 8; ++t)
@@ -702,7 +709,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 #pragma unroll
                             for (int t = 0; t < 8; ++t) {
                                 const int32_t ri = ((pos + (u0 + t) * 64) & (kGE - 1)) + lane;
-                                rw[t] = u0 + t < nu ? S.erow[ri] : 0xFF;
+                                rw[t] = S.erow[ri] | gram_pad(u0 + t, nu);
                                 cl[t] = S.ecol[ri];
                                 vl[t] = ring_val(S, ri);
                             }
@@ -793,7 +800,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             double gcur[kGB];
 #pragma unroll
             for (int i = 0; i < kGB; ++i) gcur[i] = MODE != MODE_MBCD ? S.gring[g % kGGt][i][lane] : 0.0;
-            double* cfo = S.coef + (g % kGRing) * kGB;
+            double* cfo = S.coef + (g % kGRing) * (2 * kGB);
             const int slot0 = q4 * kGB;
             // this batch's records in the lanes of its quarter (lane slot0 + i holds step
             // i, next to its accumulator): every step evaluates the update rule on all
