@@ -141,6 +141,7 @@ struct GramLds {
 };
 static_assert(sizeof(GramLds) * 2 <= 160 * 1024, "gram_kernel LDS: two workgroups per CU");
 static_assert(kGramThreads == 512, "gram_kernel's hot part gives each of the 8 waves two updaters");
+static_assert(kGramNU % 4 == 0, "gram_kernel probes four units at a time");
 
 __device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 21; }  // 11 bits
 
@@ -267,26 +268,66 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
         }
         __syncthreads();
         phase(5);
+        // entries of updater rows of column c from i on (list order), into partner pp
+        auto walk = [&](int32_t i, int pp, double v) {
+            for (; i >= 0; i = L.enext[i]) {
+                const int uu = L.eu[i];
+                if (pp > uu) atomicAdd(&L.acc[uu][pp], v * L.eval[i]);
+            }
+        };
         for (int32_t qa = 0; qa < T; qa += kGramCH) {
             load(qa);
+            // four units at a time, in dependent rounds whose LDS reads go out
+            // together: the home slot (key, head), the head entry (most cold columns
+            // have one updater entry), then the rare rest one unit at a time
+            // (longer lists, and probes that met another key)
 #pragma unroll
-            for (int u = 0; u < kGramNU; ++u) {
-                const int32_t c = cc[u];
-                if (c < kGHot) continue;
-                const int pp = owner_of(u);
-                if (pp == 0) continue;  // no updater before partner 0
-                uint32_t h = gram_hash(c) & (kGramTable - 1);
-                for (;;) {
-                    const int32_t key = L.tkey[h];
-                    if (key == c) {
-                        for (int32_t i = L.thead[h]; i >= 0; i = L.enext[i]) {
-                            const int uu = L.eu[i];
-                            if (pp > uu) atomicAdd(&L.acc[uu][pp], vv[u] * L.eval[i]);
+            for (int u0 = 0; u0 < kGramNU; u0 += 4) {
+                uint32_t h[4];
+                int32_t key[4], hd[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    h[t] = gram_hash(cc[u0 + t]) & (kGramTable - 1);
+                    key[t] = L.tkey[h[t]];
+                    hd[t] = L.thead[h[t]];
+                }
+                bool act[4], hit[4];
+                int32_t nx[4];
+                int eu[4];
+                double ev[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int u = u0 + t;
+                    act[t] = cc[u] >= kGHot && owner_of(u) != 0;  // no updater before partner 0
+                    hit[t] = act[t] && key[t] == cc[u];
+                    const int32_t i0 = hit[t] ? hd[t] : 0;
+                    ev[t] = L.eval[i0];
+                    eu[t] = L.eu[i0];
+                    nx[t] = L.enext[i0];
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int u = u0 + t, pp = owner_of(u);
+                    if (hit[t] && pp > eu[t]) atomicAdd(&L.acc[eu[t]][pp], vv[u] * ev[t]);
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int u = u0 + t, pp = owner_of(u);
+                    const int32_t c = cc[u];
+                    if (hit[t]) {
+                        if (nx[t] >= 0) walk(nx[t], pp, vv[u]);
+                    } else if (act[t] && key[t] != -1) {
+                        uint32_t hh = (h[t] + 1) & (kGramTable - 1);
+                        for (;;) {
+                            const int32_t k2 = L.tkey[hh];
+                            if (k2 == c) {
+                                walk(L.thead[hh], pp, vv[u]);
+                                break;
+                            }
+                            if (k2 == -1) break;
+                            hh = (hh + 1) & (kGramTable - 1);
                         }
-                        break;
                     }
-                    if (key == -1) break;
-                    h = (h + 1) & (kGramTable - 1);
                 }
             }
         }
