@@ -372,6 +372,8 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
 // B = 0, E = -1.  MbCD (MinibatchCD.scala:104): A = 0, so B = 0.
 constexpr int kGWin = kGSlots + kGB;     // loader's look-back for alpha forwarding: 5 batches
 constexpr int kGE = 8192;                // staged entries (LDS ring positions)
+constexpr int kGUnitB = 64 * 13;         // bytes of one 64-entry ring unit
+constexpr int kGOCol = 0, kGOLo = 256, kGOHi = 512, kGORow = 768;  // its fields
 constexpr int kGMaxU = 32;               // 64-entry units of a staged batch; larger batches go direct
 constexpr int kGFetch = 2;               // fetch waves
 constexpr int kGThreads = 64 * (3 + kGFetch);
@@ -406,9 +408,11 @@ struct GramSolverLds {
     double part[kGB + 1][64];          // memory wave: per-lane row partial sums of a batch's products (+ a sink row)
     double gring[kGGt][kGB][kGSlots];  // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
     int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
-    int32_t ecol[kGE];                 // staged entries (fetch waves -> memory wave): column,
-    uint32_t evlo[kGE], evhi[kGE];     //   value (two halves: the LDS DMA moves 4 bytes a lane),
-    uint8_t erow[kGE];                 //   row in the batch (0xFF: past the batch's entries)
+    // staged entries (fetch waves -> memory wave), 64 per ring unit: columns, value
+    // low words, value high words (the LDS DMA moves 4 bytes a lane), row bytes
+    // (0xFF: past the batch's entries).  One address per lane and unit reaches all
+    // four (immediate offsets; the two value words in one ds_read2).
+    alignas(16) uint8_t ring[kGE / 64][kGUnitB];
 };
 
 static_assert(sizeof(GramSolverLds) <= 160 * 1024, "solver_gram_kernel LDS");
@@ -450,8 +454,15 @@ __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
 __device__ __forceinline__ uint32_t gram_pad(int32_t u, int32_t nu) {
     return (uint32_t)((nu - 1 - u) >> 31) & 0xFFu;
 }
-__device__ __forceinline__ double ring_val(const GramSolverLds& S, int32_t ri) {
-    return __hiloint2double((int)S.evhi[ri], (int)S.evlo[ri]);
+// ring unit of entry position pos (a multiple of 64) + 64 u
+__device__ __forceinline__ int32_t ring_unit(int32_t pos, int32_t u) { return ((pos >> 6) + u) & (kGE / 64 - 1); }
+// lane's entry of a ring unit: (column, value, row byte)
+__device__ __forceinline__ void ring_get(const GramSolverLds& S, int32_t us, int lane, int32_t& col, double& val,
+                                         uint32_t& row) {
+    const uint8_t* b = S.ring[us];
+    col = *(const int32_t*)(b + kGOCol + 4 * lane);
+    val = __hiloint2double(*(const int*)(b + kGOHi + 4 * lane), *(const int*)(b + kGOLo + 4 * lane));
+    row = b[kGORow + lane];
 }
 
 // Roles (kGThreads threads, one workgroup per partition):
@@ -608,15 +619,15 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 if (!wait_ge(&S.cnt[kCFreed], pos + nu * 64 - kGE, abortf, a.status, pw)) break;
                 for (int32_t u = 0; u < nu; ++u) {
                     const int32_t q = u * 64 + lane;
-                    const int32_t ri = (pos + u * 64) & (kGE - 1);
+                    uint8_t* ub = S.ring[ring_unit(pos, u)];
                     const int o = gram_owner(L.sx, q);
                     if (q < T) {
                         const int64_t e = L.sb[o] + (q - L.sx[o]);
-                        lds_dma4(a.col + e, S.ecol + ri);
-                        lds_dma4((const uint32_t*)(a.val + e), S.evlo + ri);
-                        lds_dma4((const uint32_t*)(a.val + e) + 1, S.evhi + ri);
+                        lds_dma4(a.col + e, ub + kGOCol);
+                        lds_dma4((const uint32_t*)(a.val + e), ub + kGOLo);
+                        lds_dma4((const uint32_t*)(a.val + e) + 1, ub + kGOHi);
                     }
-                    S.erow[ri + lane] = q < T ? (uint8_t)o : (uint8_t)0xFF;
+                    ub[kGORow + lane] = q < T ? (uint8_t)o : (uint8_t)0xFF;
                 }
                 vm_drain();  // the DMA writes are in LDS
             }
@@ -691,7 +702,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 const int32_t pos = L.pos, nu = L.nu;
                 if (pos >= 0) {
                     if (!fetched(b)) break;
-                    // groups of 4 units: the LDS reads of a group go out together (reading
+                    // groups of 8 units: the LDS reads of a group go out together (reading
                     // past the batch is harmless: those lanes get row 0xFF)
                     // (every read of a group before its first atomic: an LDS atomic may
                     // alias them in the compiler's view and would serialise the group)
@@ -701,10 +712,9 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         double vl[8], cc[8];
 #pragma unroll
                         for (int t = 0; t < 8; ++t) {
-                            const int32_t ri = ((pos + (u0 + t) * 64) & (kGE - 1)) + lane;
-                            rw[t] = S.erow[ri] | gram_pad(u0 + t, nu);
-                            cl[t] = S.ecol[ri];
-                            vl[t] = ring_val(S, ri);
+                            uint32_t r8;
+                            ring_get(S, ring_unit(pos, u0 + t), lane, cl[t], vl[t], r8);
+                            rw[t] = r8 | gram_pad(u0 + t, nu);
                         }
 #pragma unroll
                         for (int t = 0; t < 8; ++t) cc[t] = cf[rw[t] & (2 * kGB - 1)];  // row 0xFF: a zero slot
@@ -749,10 +759,9 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                             double vl[8];
 #pragma unroll
                             for (int t = 0; t < 8; ++t) {
-                                const int32_t ri = ((pos + (u0 + t) * 64) & (kGE - 1)) + lane;
-                                rw[t] = S.erow[ri] | gram_pad(u0 + t, nu);
-                                cl[t] = S.ecol[ri];
-                                vl[t] = ring_val(S, ri);
+                                uint32_t r8;
+                                ring_get(S, ring_unit(pos, u0 + t), lane, cl[t], vl[t], r8);
+                                rw[t] = r8 | gram_pad(u0 + t, nu);
                             }
                             double hx[8];
 #pragma unroll
