@@ -121,8 +121,8 @@ __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F
 //     updaters' cold entries, filled tile by tile (kGramTile packed positions
 //     of the updater rows at a time); every partner cold entry probes it.
 // Windows longer than the register chunk reload it per tile (same results).
-constexpr int kGramTable = 2048;     // hash slots (power of two, 2 x kGramTile)
-constexpr int kGramTile = 1024;      // updater positions per hash tile
+constexpr int kGramTable = 4096;     // hash slots (power of two, 2 x kGramTile)
+constexpr int kGramTile = 2048;      // updater positions per hash tile (16 rows of ~128 entries: one tile)
 constexpr int kGramThreads = 512;    // 8 waves: two workgroups (53 KB of LDS each) give 16 waves per CU
 constexpr int kGramNU = 12;          // kGramThreads-entry units in registers
 constexpr int kGramCH = kGramNU * kGramThreads;
@@ -143,7 +143,8 @@ static_assert(sizeof(GramLds) * 2 <= 160 * 1024, "gram_kernel LDS: two workgroup
 static_assert(kGramThreads == 512, "gram_kernel's hot part gives each of the 8 waves two updaters");
 static_assert(kGramNU % 4 == 0, "gram_kernel probes four units at a time");
 
-__device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 21; }  // 11 bits
+__device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 20; }  // 12 bits
+static_assert(kGramTable == 4096 && kGramTile <= 32767, "gram_hash bits / int16 list links");
 
 __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
