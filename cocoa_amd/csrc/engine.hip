@@ -1491,6 +1491,7 @@ extern "C" int cocoa_get_w(cocoa_ctx* ctx, double* w_out) {
     std::vector<double> dev((size_t)ctx->d);
     HIPCHK(hipMemcpyAsync(dev.data(), ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    check_status(ctx);
     ctx->to_host_order(dev, w_out);
     CAPI_END(ctx)
 }
@@ -1502,6 +1503,7 @@ extern "C" int cocoa_get_alpha(cocoa_ctx* ctx, double* alpha_out) {
         HIPCHK(hipMemcpyAsync(alpha_out, ctx->alpha.p, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyDeviceToHost,
                               ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    check_status(ctx);
     CAPI_END(ctx)
 }
 
