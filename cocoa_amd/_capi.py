@@ -86,6 +86,8 @@ _pi32, _pi64, _pf64 = ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_in
 SIGNATURES = {
     "cocoa_version": (_int, []),
     "cocoa_create": (_int, [_int, _int, _vp, ctypes.POINTER(_vp)]),
+    "cocoa_create_multi": (_int, [_i32, _pi32, _int, ctypes.POINTER(_vp)]),
+    "cocoa_num_devices": (_int, [_vp, _pi32, _pi32, _i32]),
     "cocoa_destroy": (_int, [_vp]),
     "cocoa_last_error": (ctypes.c_char_p, [_vp]),
     "cocoa_set_train": (_int, [_vp, _i32, _pi64, _pi64, _pi32, _pf64, _pf64, _i64, _i32, _i32, _i32]),
@@ -137,7 +139,7 @@ SIGNATURES = {
     "cocoa_comm_ordered_sum": (_int, [_vp, _pf64, _i64]),
 }
 
-TRANSPORTS = {"rccl": 0, "host": 1}
+TRANSPORTS = {"rccl": 0, "host": 1, "local": 2}
 UID_BYTES = 128
 
 _lib = None

@@ -89,19 +89,39 @@ static_assert(sizeof(HostUid) <= (size_t)kUidBytes, "uid layout");
 std::mutex g_listen_mu;
 std::map<uint64_t, int> g_listen;  // nonce -> listening socket of this process
 
+// Connect / handshake timeout (COCOA_COMM_TIMEOUT_MS, default 120 s).
 int timeout_ms() {
     const char* e = std::getenv("COCOA_COMM_TIMEOUT_MS");
     return e ? std::atoi(e) : 120000;
+}
+// Exchange timeout (COCOA_COMM_EXCHANGE_TIMEOUT_MS, default 0 = none): a
+// round's recv also waits for the other ranks' work -- the strict chain, rank
+// 0's relay, ranks that finish set_train / the compact layout at different
+// times -- which on C4-sized data can outlast any handshake-sized limit.
+int exchange_timeout_ms() {
+    const char* e = std::getenv("COCOA_COMM_EXCHANGE_TIMEOUT_MS");
+    return e ? std::atoi(e) : 0;
+}
+
+timeval to_timeval(int ms) {
+    timeval tv{};
+    if (ms > 0) {
+        tv.tv_sec = ms / 1000;
+        tv.tv_usec = (ms % 1000) * 1000;
+    }
+    return tv;  // {0, 0}: no timeout
+}
+
+void set_sock_timeout(int fd, int ms) {
+    const timeval tv = to_timeval(ms);
+    (void)setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    (void)setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
 }
 
 void set_sock_opts(int fd) {
     const int one = 1;
     (void)setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-    timeval tv{};
-    tv.tv_sec = timeout_ms() / 1000;
-    tv.tv_usec = (timeout_ms() % 1000) * 1000;
-    (void)setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
-    (void)setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    set_sock_timeout(fd, timeout_ms());  // the handshake; exchange_timeout_ms() once connected
 }
 
 }  // namespace
@@ -177,8 +197,7 @@ Comm* comm_create(int transport, int rank, int world, const void* uid, int devic
                 }
                 if (lfd < 0) throw Error(COCOA_E_ARG, "rank 0 must create the HOST uid (cocoa_comm_unique_id)");
                 c->fds.assign((size_t)world, -1);
-                timeval tv{};
-                tv.tv_sec = timeout_ms() / 1000;
+                const timeval tv = to_timeval(timeout_ms());
                 (void)setsockopt(lfd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
                 for (int got = 1; got < world; ++got) {
                     const int fd = accept(lfd, nullptr, nullptr);
@@ -204,6 +223,8 @@ Comm* comm_create(int transport, int rank, int world, const void* uid, int devic
                     c->fds[(size_t)hello[0]] = fd;
                 }
                 close(lfd);
+                for (int fd : c->fds)
+                    if (fd >= 0) set_sock_timeout(fd, exchange_timeout_ms());
             } else {
                 sockaddr_in sa{};
                 sa.sin_family = AF_INET;
@@ -223,6 +244,7 @@ Comm* comm_create(int transport, int rank, int world, const void* uid, int devic
                 const int32_t hello[3] = {rank, (int32_t)(uint32_t)u.nonce, (int32_t)(uint32_t)(u.nonce >> 32)};
                 c->fds.assign(1, fd);
                 c->host_send(fd, hello, sizeof hello);
+                set_sock_timeout(fd, exchange_timeout_ms());
             }
         } else {
             throw Error(COCOA_E_ARG, "unknown transport");

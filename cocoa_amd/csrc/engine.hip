@@ -79,7 +79,28 @@ struct Csr {
     int64_t n = 0, nnz = 0;
     DevBuf row_ptr, col, val, y;
     DevBuf col16;  // uint16 copy of col when d <= 65,536 (fast eval stream), else empty
+    // dense rows set through cocoa_set_*_dense: no column array until a CSR
+    // kernel needs one (ensure_cols builds it on the device)
+    bool col_lazy = false;
 };
+
+// the column arrays of dense rows (entry q is column q mod d; device order is
+// the identity for dense rows), built on the device when first needed
+void ensure_cols(Csr& c, int32_t d, hipStream_t s) {
+    if (!c.col_lazy) return;
+    c.col.alloc(sizeof(int32_t) * (size_t)c.nnz + 64);
+    HIPCHK(hipMemsetAsync((char*)c.col.p + sizeof(int32_t) * (size_t)c.nnz, 0, 64, s));
+    if (d <= 65536) {
+        c.col16.alloc(sizeof(uint16_t) * (size_t)c.nnz + 64);
+        HIPCHK(hipMemsetAsync((char*)c.col16.p + sizeof(uint16_t) * (size_t)c.nnz, 0, 64, s));
+    } else {
+        c.col16.free();
+    }
+    cocoa::launch_dense_cols(c.col.as<int32_t>(), c.col16.p ? c.col16.as<uint16_t>() : nullptr, c.nnz, d, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    c.col_lazy = false;
+}
 
 // uint16 column copy for the fast eval when every device column fits 16 bits
 void upload_col16(DevBuf& b, const std::vector<int32_t>& pcol, int64_t nnz, int32_t d, hipStream_t s) {
@@ -109,6 +130,20 @@ struct cocoa_comm {
 struct cocoa_ctx {
     int device = 0;
     bool strict = false;
+    // Multi-device context (cocoa_create_multi): one sub-context per device,
+    // each holding a contiguous block of the partitions, all driven from the
+    // caller's thread; the exchange between them runs on the devices' streams
+    // (peer copies + an ordered sum).  The group itself holds no device data,
+    // only the problem's shape (d, K, rows, params) for the objectives and
+    // checkpoints.
+    std::vector<cocoa_ctx*> subs;
+    std::vector<int32_t> g_k0;        // first partition of each sub (+ K at the end)
+    std::vector<int64_t> g_r0;        // first training row of each sub (+ n)
+    std::vector<int64_t> g_t0;        // first test row of each sub (+ n_test)
+    DevBuf g_stage;                   // fast exchange: the other subs' sums, on subs[0]'s device
+    std::vector<hipEvent_t> g_ev;     // per sub: its sum (its part of the chain, or the total) is ready
+    std::vector<hipEvent_t> g_ev_cp;  // per sub: it has copied the total
+    bool is_group() const { return !subs.empty(); }
     // rank exchange (cocoa_comm_init): owned; null = single rank / caller-driven
     cocoa::Comm* comm = nullptr;
     hipStream_t stream = nullptr;
@@ -169,6 +204,11 @@ struct cocoa_ctx {
     cocoa_params P{};
     cocoa_debug D{};
     double scaling = 1.0, mult = 1.0;
+    // alpha set from outside [0, 1] (cocoa_set_alpha / checkpoint): with it, or
+    // with a scaling outside [0, 1], the fast SDCA solvers run the explicit
+    // projected-gradient skip test (CoCoA.scala:166-172) instead of the clamp alone
+    bool alpha_oob = false;
+    bool proj_rule() const { return alpha_oob || scaling < 0.0 || scaling > 1.0; }
     DevBuf w, alpha, alpha_work, dw, wloc, samples, dw_sum_int, eval_part, eval_out, row_scratch, jump, prof;
     double* dw_sum = nullptr;
     double* h_eval = nullptr;  // pinned [4]
@@ -256,6 +296,16 @@ struct cocoa_ctx {
         pending.clear();
     }
     ~cocoa_ctx() {
+        for (size_t r = 0; r < subs.size(); ++r) {
+            (void)hipSetDevice(subs[r]->device);
+            if (r < g_ev.size() && g_ev[r]) (void)hipEventDestroy(g_ev[r]);
+            if (r < g_ev_cp.size() && g_ev_cp[r]) (void)hipEventDestroy(g_ev_cp[r]);
+            delete subs[r];
+        }
+        if (!subs.empty()) {
+            (void)hipSetDevice(device);
+            g_stage.free();
+        }
         if (stream) (void)hipStreamSynchronize(stream);
         if (gstream) {
             (void)hipStreamSynchronize(gstream);
@@ -304,6 +354,22 @@ struct cocoa_ctx {
 static void require(bool cond, int code, const std::string& msg) {
     if (!cond) throw Error(code, msg);
 }
+
+// multi-device contexts (cocoa_create_multi): the group side of the entry points
+static void group_set_train(cocoa_ctx* g, int32_t K, const int64_t* part_ptr, const int64_t* row_ptr,
+                            const int32_t* col, const double* val, const double* y, int64_t n, int32_t d,
+                            int32_t part_begin, int32_t Kg);
+static void group_set_test(cocoa_ctx* g, const int64_t* row_ptr, const int32_t* col, const double* val,
+                           const double* y, int64_t n_rows);
+static void group_init(cocoa_ctx* g, const cocoa_params* params, const cocoa_debug* debug, int method,
+                       const double* w_init);
+static void group_round(cocoa_ctx* g, int32_t t);
+static void group_get_state(cocoa_ctx* g, double* w, double* alpha);
+static void group_set_state(cocoa_ctx* g, const double* w, const double* alpha);
+static int32_t group_owner_of_part(const cocoa_ctx* g, int32_t part);
+static void sub_check(int rc, const cocoa_ctx* sub);
+#define GROUP_REJECT(ctx, what) \
+    require(!(ctx)->is_group(), COCOA_E_STATE, what " is not available on a multi-device context (it exchanges internally)")
 
 // after a stream synchronisation: a Gram-solver launch that had to abort
 static void check_status(cocoa_ctx* c) {
@@ -439,14 +505,11 @@ static bool is_dense(const int64_t* row_ptr, const int32_t* col, int64_t n, int3
     return true;
 }
 
-// CSR view of a dense matrix (the column array is the only new storage)
-static void dense_csr(int64_t n, int32_t d, std::vector<int64_t>& rp, std::vector<int32_t>& col) {
-    rp.resize((size_t)n + 1);
-    for (int64_t r = 0; r <= n; ++r) rp[(size_t)r] = r * (int64_t)d;
-    col.resize((size_t)std::max<int64_t>(n * (int64_t)d, 1));
-    for (int64_t r = 0; r < n; ++r)
-        for (int32_t j = 0; j < d; ++j) col[(size_t)(r * (int64_t)d + j)] = j;
-}
+static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const int64_t* row_ptr,
+                           const int32_t* col, const double* val, const double* y, int64_t n_rows,
+                           int32_t num_features, int32_t part_begin, int32_t num_parts_global);
+static void set_test_impl(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t* col, const double* val,
+                          const double* y, int64_t n_rows);
 
 // Compact deltaW layout (see cocoa_ctx::compact_ready).  COCOA_DW_COMPACT=0 / 1
 // forces it off / on (tests); on by default once K_loc * d * 8 >= 1 GiB and the
@@ -515,17 +578,17 @@ extern "C" int cocoa_set_train_dense(cocoa_ctx* ctx, int32_t num_parts, const in
         cocoa_set_global_error(ctx->err);
         return COCOA_E_ARG;
     }
-    std::vector<int64_t> rp;
-    std::vector<int32_t> col;
-    try {
-        dense_csr(n_rows, num_features, rp, col);
-    } catch (const std::exception& e) {
-        ctx->err = std::string("cocoa_set_train_dense: ") + e.what();
-        cocoa_set_global_error(ctx->err);
-        return COCOA_E_ARG;
+    CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        group_set_train(ctx, num_parts, part_ptr, nullptr, nullptr, X, y, n_rows, num_features, part_begin,
+                        num_parts_global);
+        return COCOA_OK;
     }
-    return cocoa_set_train(ctx, num_parts, part_ptr, rp.data(), col.data(), X, y, n_rows, num_features, part_begin,
-                           num_parts_global);
+    std::vector<int64_t> rp((size_t)n_rows + 1);
+    for (int64_t r = 0; r <= n_rows; ++r) rp[(size_t)r] = r * (int64_t)num_features;
+    set_train_impl(ctx, num_parts, part_ptr, rp.data(), nullptr, X, y, n_rows, num_features, part_begin,
+                   num_parts_global);
+    CAPI_END(ctx)
 }
 
 extern "C" int cocoa_set_test_dense(cocoa_ctx* ctx, const double* X, const double* y, int64_t n_rows) {
@@ -535,22 +598,39 @@ extern "C" int cocoa_set_test_dense(cocoa_ctx* ctx, const double* X, const doubl
         cocoa_set_global_error(ctx->err);
         return ctx->d < 1 ? COCOA_E_STATE : COCOA_E_ARG;
     }
-    std::vector<int64_t> rp;
-    std::vector<int32_t> col;
-    try {
-        dense_csr(n_rows, ctx->d, rp, col);
-    } catch (const std::exception& e) {
-        ctx->err = std::string("cocoa_set_test_dense: ") + e.what();
-        cocoa_set_global_error(ctx->err);
-        return COCOA_E_ARG;
+    CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        group_set_test(ctx, nullptr, nullptr, X, y, n_rows);
+        return COCOA_OK;
     }
-    return cocoa_set_test(ctx, rp.data(), col.data(), X, y, n_rows);
+    std::vector<int64_t> rp((size_t)n_rows + 1);
+    for (int64_t r = 0; r <= n_rows; ++r) rp[(size_t)r] = r * (int64_t)ctx->d;
+    set_test_impl(ctx, rp.data(), nullptr, X, y, n_rows);
+    CAPI_END(ctx)
 }
 
 extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const int64_t* row_ptr,
                                const int32_t* col, const double* val, const double* y, int64_t n_rows,
                                int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
     CAPI_BEGIN(ctx)
+    require(col != nullptr || (row_ptr && n_rows >= 0 && row_ptr[n_rows] == 0), COCOA_E_ARG,
+            "cocoa_set_train: null column array");
+    if (ctx->is_group()) {
+        static const int32_t no_col = 0;  // CSR (possibly empty), not the dense marker
+        group_set_train(ctx, num_parts, part_ptr, row_ptr, col ? col : &no_col, val, y, n_rows, num_features,
+                        part_begin, num_parts_global);
+        return COCOA_OK;
+    }
+    set_train_impl(ctx, num_parts, part_ptr, row_ptr, col, val, y, n_rows, num_features, part_begin,
+                   num_parts_global);
+    CAPI_END(ctx)
+}
+
+// col == nullptr: dense rows (row r = columns 0..d-1 at entries [r d, (r+1) d))
+static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const int64_t* row_ptr,
+                           const int32_t* col, const double* val, const double* y, int64_t n_rows,
+                           int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
+    const bool dense_in = col == nullptr;
     ctx->gram_quiesce();  // a Gram prefetch reads the CSR being replaced
     require(num_parts >= 1 && part_ptr && row_ptr && y && n_rows >= 0 && num_features >= 1, COCOA_E_ARG,
             "cocoa_set_train: bad argument");
@@ -558,9 +638,10 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
             "cocoa_set_train: bad partition range");
     require(part_ptr[0] == 0 && part_ptr[num_parts] == n_rows, COCOA_E_ARG, "part_ptr must span [0, n_rows]");
     for (int k = 0; k < num_parts; ++k) require(part_ptr[k + 1] >= part_ptr[k], COCOA_E_ARG, "part_ptr not monotone");
-    check_csr(row_ptr, col, n_rows, num_features);
+    if (!dense_in) check_csr(row_ptr, col, n_rows, num_features);
     const int64_t nnz = row_ptr[n_rows];
-    ctx->tr_dense = is_dense(row_ptr, col, n_rows, num_features);
+    require(val != nullptr || nnz == 0, COCOA_E_ARG, "cocoa_set_train: null value array");
+    ctx->tr_dense = dense_in ? n_rows >= 1 : is_dense(row_ptr, col, n_rows, num_features);
     ctx->K_loc = num_parts;
     ctx->K_glob = num_parts_global;
     ctx->part_begin = part_begin;
@@ -589,7 +670,7 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
         bool sorted = true;
         for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) {
             s += val[q] * val[q];
-            if (q > row_ptr[r] && col[q] <= col[q - 1]) sorted = false;
+            if (!dense_in && q > row_ptr[r] && col[q] <= col[q - 1]) sorted = false;
         }
         const double nr = std::sqrt(s);
         sq[(size_t)r] = nr * nr;
@@ -608,7 +689,10 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     // order; w crosses the C ABI in the original order.
     {
         std::vector<int64_t> freq((size_t)num_features, 0);
-        for (int64_t q = 0; q < nnz; ++q) freq[(size_t)col[q]]++;
+        if (dense_in)  // every column n_rows times: the identity order
+            std::fill(freq.begin(), freq.end(), n_rows);
+        else
+            for (int64_t q = 0; q < nnz; ++q) freq[(size_t)col[q]]++;
         std::vector<int32_t> order((size_t)num_features);
         for (int32_t j = 0; j < num_features; ++j) order[(size_t)j] = j;
         std::stable_sort(order.begin(), order.end(),
@@ -620,42 +704,79 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
         for (int32_t j = 0; j < num_features; ++j)
             ctx->n_hot_nnz[(size_t)j + 1] = ctx->n_hot_nnz[(size_t)j] + freq[(size_t)order[(size_t)j]];
     }
-    std::vector<int32_t> pcol((size_t)std::max<int64_t>(nnz, 1));
-    for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];
+    std::vector<int32_t> pcol;
+    if (!dense_in) {
+        pcol.resize((size_t)std::max<int64_t>(nnz, 1));
+        for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];
+    }
     hipStream_t s = ctx->stream;
     upload(ctx->d_perm, ctx->perm.data(), sizeof(int32_t) * (size_t)num_features, s);
     upload(ctx->d_inv, ctx->inv.data(), sizeof(int32_t) * (size_t)num_features, s);
     upload(ctx->tr.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
-    upload_padded(ctx->tr.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
-    upload_col16(ctx->tr.col16, pcol, nnz, num_features, s);
+    ctx->tr.col_lazy = dense_in;
+    if (dense_in) {
+        ctx->tr.col.free();
+        ctx->tr.col16.free();
+    } else {
+        upload_padded(ctx->tr.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
+        upload_col16(ctx->tr.col16, pcol, nnz, num_features, s);
+    }
     upload_padded(ctx->tr.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s, eval_tile_entries());
-    build_compact(ctx, row_ptr, pcol.data());
+    if (dense_in) {
+        ctx->compact_ready = false;  // dense rows touch every column: no compact slices
+        ctx->col_local.free();
+        ctx->fptr.free();
+        ctx->fpos.free();
+    } else {
+        build_compact(ctx, row_ptr, pcol.data());
+    }
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
-    CAPI_END(ctx)
 }
 
 extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t* col, const double* val,
                               const double* y, int64_t n_rows) {
     CAPI_BEGIN(ctx)
+    require(col != nullptr || (row_ptr && n_rows >= 0 && row_ptr[n_rows] == 0), COCOA_E_ARG,
+            "cocoa_set_test: null column array");
+    if (ctx->is_group()) {
+        static const int32_t no_col = 0;
+        group_set_test(ctx, row_ptr, col ? col : &no_col, val, y, n_rows);
+        return COCOA_OK;
+    }
+    set_test_impl(ctx, row_ptr, col, val, y, n_rows);
+    CAPI_END(ctx)
+}
+
+// col == nullptr: dense rows
+static void set_test_impl(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t* col, const double* val,
+                          const double* y, int64_t n_rows) {
+    const bool dense_in = col == nullptr;
     require(ctx->d > 0, COCOA_E_STATE, "cocoa_set_test: call cocoa_set_train first");
     require(row_ptr && y && n_rows >= 0, COCOA_E_ARG, "cocoa_set_test: bad argument");
-    check_csr(row_ptr, col, n_rows, ctx->d);
+    if (!dense_in) check_csr(row_ptr, col, n_rows, ctx->d);
     const int64_t nnz = row_ptr[n_rows];
+    require(val != nullptr || nnz == 0, COCOA_E_ARG, "cocoa_set_test: null value array");
     hipStream_t s = ctx->stream;
-    ctx->te_dense = is_dense(row_ptr, col, n_rows, ctx->d);
+    ctx->te_dense = dense_in ? n_rows >= 1 : is_dense(row_ptr, col, n_rows, ctx->d);
     ctx->te.n = n_rows;
     ctx->te.nnz = nnz;
-    std::vector<int32_t> pcol((size_t)std::max<int64_t>(nnz, 1));
-    for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];  // device feature order
     upload(ctx->te.row_ptr, row_ptr, sizeof(int64_t) * (size_t)(n_rows + 1), s);
-    upload_padded(ctx->te.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
-    upload_col16(ctx->te.col16, pcol, nnz, ctx->d, s);
+    ctx->te.col_lazy = dense_in;
+    if (dense_in) {
+        ctx->te.col.free();
+        ctx->te.col16.free();
+    } else {
+        std::vector<int32_t> pcol((size_t)std::max<int64_t>(nnz, 1));
+        for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];  // device feature order
+        upload_padded(ctx->te.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
+        upload_col16(ctx->te.col16, pcol, nnz, ctx->d, s);
+    }
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s, eval_tile_entries());
@@ -665,7 +786,6 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
         const size_t rows = (size_t)(ctx->tr.n + ctx->te.n);
         ctx->row_scratch.alloc(sizeof(double) * std::max<size_t>(rows, 1));
     }
-    CAPI_END(ctx)
 }
 
 // ----------------------------------------------------------------- solver --
@@ -736,12 +856,17 @@ extern "C" int cocoa_set_solver(cocoa_ctx* ctx, int kind) {
             COCOA_E_ARG, "cocoa_set_solver: unknown solver");
     ctx->solver_kind = kind;
     ctx->inited = false;  // takes effect at the next cocoa_init
+    for (cocoa_ctx* sub : ctx->subs) sub_check(cocoa_set_solver(sub, kind), sub);
     CAPI_END(ctx)
 }
 
 extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
                           const double* w_init) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        group_init(ctx, params, debug, method, w_init);
+        return COCOA_OK;
+    }
     require(params && method >= 0 && method <= 4, COCOA_E_ARG, "cocoa_init: bad argument");
     require(ctx->d > 0 && ctx->K_loc > 0, COCOA_E_STATE, "cocoa_init: no training data");
     require(params->local_iters >= 0 && params->n >= 1, COCOA_E_ARG, "cocoa_init: bad params");
@@ -773,6 +898,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     } else
         HIPCHK(hipMemsetAsync(ctx->w.p, 0, sizeof(double) * (size_t)d, s));
     ctx->alpha.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
+    ctx->alpha_oob = false;
     ctx->alpha_work.alloc(sizeof(double) * (size_t)(std::max<int64_t>(n, 1) + K));  // + a sink per partition
     if (ctx->zstream) HIPCHK(hipStreamSynchronize(ctx->zstream));  // no re-zeroing in flight
     ctx->gram_quiesce();                                            // no Gram prefetch in flight
@@ -864,6 +990,12 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     // (measured: 46 ms per C4 round on the side stream) only compete with them.
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    // every local solver but the dense one reads the column array (and the
+    // dense rows of cocoa_set_train_dense have none yet)
+    if (ctx->strict || !ctx->use_dense) {
+        ensure_cols(ctx->tr, ctx->d, s);
+        a.col = ctx->dw_compact ? ctx->col_local.as<int32_t>() : ctx->tr.col.as<int32_t>();
+    }
     ctx->use_gram = !ctx->strict && !ctx->use_dense && is_sdca(method) && H >= 1 &&
                     (ctx->solver_kind == COCOA_SOLVER_GRAM ||
                      (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0 && K <= ncu));
@@ -953,8 +1085,12 @@ static GramArgs gram_args(cocoa_ctx* c, const int32_t* samples, double* gt) {
 }
 
 // fuse_apply: w += sum * mult inside the fold (one rank, no exchange).
-// chain_init: strict multi-rank fold, continuing the previous ranks' fold.
-static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* chain_init = nullptr) {
+// chain_init: strict multi-rank fold, continuing the previous ranks' fold,
+// which recv_init (a multi-device context's peer copy) or the communicator's
+// chain_recv puts into dw_sum first.
+typedef void (*recv_fn)(cocoa_ctx* c, void* user);
+static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* chain_init = nullptr,
+                      recv_fn recv_init = nullptr, void* recv_user = nullptr) {
     require(c->inited, COCOA_E_STATE, "cocoa_round: call cocoa_init first");
     const int32_t H = c->P.local_iters;
     const int32_t seed = wrap32((int64_t)c->D.seed + t);                    // debug.seed + t
@@ -1050,6 +1186,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.inv_lam_n = 1.0 / c->sa.lam_n;
             g.sigma = c->method == COCOA_METHOD_COCOA_PLUS ? c->sa.sigma : 1.0;
             g.scaling = c->scaling;
+            g.proj = c->proj_rule() ? 1 : 0;
             c->timed(COCOA_K_SOLVER, [&] { launch_solver_dense(solver_mode(c->method), g, K, c->max_nl, s); });
         } else if (c->use_gram) {
             GramSolverArgs g{};
@@ -1076,6 +1213,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.inv_lam_n = 1.0 / c->sa.lam_n;
             g.sigma = c->method == COCOA_METHOD_COCOA_PLUS ? c->sa.sigma : 1.0;
             g.scaling = c->scaling;
+            g.proj = c->proj_rule() ? 1 : 0;
             c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(solver_mode(c->method), g, K, s); });
             if (overlap) {
                 // round t+1's samples and Gram rows on gstream, beside this solver (its
@@ -1126,7 +1264,12 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         c->timed(COCOA_K_APPLY, [&] { launch_scale(c->w.as<double>(), d, 1.0 - (step * c->P.lambda), s); });
         c->mult = step * c->scaling;
     }
-    if (chain_init) c->comm->chain_recv(c->dw_sum, d, true, s);  // the fold of ranks < rank (rank > 0)
+    if (chain_init) {  // the fold of ranks < rank (rank > 0)
+        if (recv_init)
+            recv_init(c, recv_user);
+        else
+            c->comm->chain_recv(c->dw_sum, d, true, s);
+    }
     c->timed(COCOA_K_FOLD, [&] {
         if (c->dw_compact)
             launch_fold_compact(dws, c->fptr.as<int64_t>(), c->fpos.as<uint32_t>(), d, c->dw_sum, c->w.as<double>(),
@@ -1141,12 +1284,14 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
 
 extern "C" int cocoa_round_local(cocoa_ctx* ctx, int32_t t) {
     CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_round_local");
     run_local(ctx, t, false);
     CAPI_END(ctx)
 }
 
 extern "C" int cocoa_dw_sum_device_ptr(cocoa_ctx* ctx, void** out) {
     CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_dw_sum_device_ptr");
     require(out != nullptr, COCOA_E_ARG, "null out");
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     *out = (void*)ctx->dw_sum;
@@ -1155,12 +1300,14 @@ extern "C" int cocoa_dw_sum_device_ptr(cocoa_ctx* ctx, void** out) {
 
 extern "C" int cocoa_set_dw_sum_buffer(cocoa_ctx* ctx, void* device_ptr) {
     CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_set_dw_sum_buffer");
     ctx->dw_sum = device_ptr ? (double*)device_ptr : ctx->dw_sum_int.as<double>();
     CAPI_END(ctx)
 }
 
 extern "C" int cocoa_round_apply(cocoa_ctx* ctx) {
     CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_round_apply");
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     ctx->timed(COCOA_K_APPLY, [&] {
         launch_apply(ctx->w.as<double>(), ctx->dw_sum, ctx->d, ctx->mult, ctx->d_inv.as<int32_t>(), ctx->stream);
@@ -1178,17 +1325,29 @@ extern "C" int cocoa_round_apply(cocoa_ctx* ctx) {
 //             the single-process partition-order fold bit for bit.
 extern "C" int cocoa_round(cocoa_ctx* ctx, int32_t t) {
     CAPI_BEGIN(ctx)
-    if (!ctx->comm) {
+    if (ctx->is_group()) {
+        group_round(ctx, t);
+    } else if (!ctx->comm) {
         run_local(ctx, t, true);
     } else {
         cocoa::Comm& cm = *ctx->comm;
         const int64_t d = ctx->d;
+        // an aborted solver launch must not send its half-updated sum to the other
+        // ranks: check the status word before every exchange (the HOST transport
+        // synchronises here anyway; over RCCL this costs one stream sync per round)
+        auto checked = [&] {
+            if (ctx->use_gram && cm.world > 1) {
+                HIPCHK(hipStreamSynchronize(ctx->stream));
+                check_status(ctx);
+            }
+        };
         if (ctx->strict && cm.world > 1) {
             run_local(ctx, t, false, cm.rank > 0 ? ctx->dw_sum : nullptr);
             cm.chain_send(ctx->dw_sum, d, true, ctx->stream);
             cm.bcast_last(ctx->dw_sum, d, true, ctx->stream);
         } else {
             run_local(ctx, t, false);
+            checked();
             cm.allreduce(ctx->dw_sum, d, true, ctx->stream);
         }
         ctx->timed(COCOA_K_APPLY, [&] {
@@ -1270,6 +1429,7 @@ extern "C" int cocoa_comm_ordered_sum(cocoa_comm* comm, double* buf, int64_t n) 
 
 extern "C" int cocoa_comm_init(cocoa_ctx* ctx, int transport, int32_t rank, int32_t world, const void* uid) {
     CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_comm_init");
     HIPCHK(hipStreamSynchronize(ctx->stream));
     delete ctx->comm;
     ctx->comm = nullptr;
@@ -1279,6 +1439,12 @@ extern "C" int cocoa_comm_init(cocoa_ctx* ctx, int transport, int32_t rank, int3
 
 extern "C" int cocoa_comm_info(cocoa_ctx* ctx, int32_t* transport, int32_t* rank, int32_t* world) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {  // the devices exchange in-process
+        if (transport) *transport = COCOA_TRANSPORT_LOCAL;
+        if (rank) *rank = 0;
+        if (world) *world = (int32_t)ctx->subs.size();
+        return COCOA_OK;
+    }
     if (transport) *transport = ctx->comm ? ctx->comm->transport : -1;
     if (rank) *rank = ctx->comm ? ctx->comm->rank : 0;
     if (world) *world = ctx->comm ? ctx->comm->world : 1;
@@ -1303,10 +1469,16 @@ static void finish(const cocoa_ctx* c, double hinge, double alpha_sum, double w2
     out->test_error = n_test > 0 ? (double)err / (double)n_test : NAN;        // OptUtils.scala:95-98
 }
 
-extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
-    CAPI_BEGIN(ctx)
-    require(out != nullptr, COCOA_E_ARG, "null out");
+// The evaluation pass of one (sub-)context, enqueued: the rank-local sums land
+// in h_eval (pinned) once the stream reaches them.
+static void eval_launch(cocoa_ctx* ctx) {
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    const bool dense_eval = !ctx->strict && ctx->tr_dense && (!ctx->has_test || ctx->te_dense || ctx->te.n == 0) &&
+                            dense_eval_fits(ctx->d);
+    if (!dense_eval) {  // the CSR passes read the column arrays
+        ensure_cols(ctx->tr, ctx->d, ctx->stream);
+        if (ctx->has_test) ensure_cols(ctx->te, ctx->d, ctx->stream);
+    }
     EvalArgs e{};
     e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     e.col = ctx->tr.col.as<int32_t>();
@@ -1338,7 +1510,7 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
             launch_eval_strict(e, ctx->stream);
         else {
             e.row_xw = ctx->row_xw.as<double>();
-            if (ctx->tr_dense && (!ctx->has_test || ctx->te_dense || ctx->te.n == 0) && dense_eval_fits(ctx->d))
+            if (dense_eval)
                 launch_eval_dense(e, ctx->stream);  // rows read as X[n][d]: 8 B per entry
             else
                 launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
@@ -1346,35 +1518,64 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
         }
     });
     HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+}
+
+struct EvalLocal {
+    double hinge, alpha_sum, w2, err, n_test;
+};
+
+// wait for eval_launch's sums
+static EvalLocal eval_collect(cocoa_ctx* ctx) {
     HIPCHK(hipStreamSynchronize(ctx->stream));
     check_status(ctx);
-    double hinge = ctx->h_eval[0], alpha_sum = ctx->h_eval[1];
-    const double w2 = ctx->h_eval[2];  // w is replicated: the same on every rank
-    double counts[2] = {ctx->h_eval[3], (double)e.n_test};
+    // w is replicated: w2 is the same on every rank
+    return EvalLocal{ctx->h_eval[0], ctx->h_eval[1], ctx->h_eval[2], ctx->h_eval[3],
+                     (double)(ctx->has_test ? ctx->te.n : 0)};
+}
+
+// Strict multi-rank evaluation: continue the partition-order merge of the
+// previous ranks (OptUtils.scala:65-84 as Spark merges partitions, in index
+// order) with this rank's per-partition partials.  carry = {hinge,
+// hinge-seen flag, alpha}; first: this is the first rank.
+static void strict_eval_carry(cocoa_ctx* ctx, bool first, double carry[3]) {
+    std::vector<double> part((size_t)2 * ctx->K_loc);
+    HIPCHK(hipMemcpyAsync(part.data(), ctx->eval_part.p, sizeof(double) * part.size(), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    bool have = carry[1] != 0.0;
+    double h = carry[0], al = carry[2];
+    for (int32_t k = 0; k < ctx->K_loc; ++k) {
+        al = (first && k == 0) ? part[2 * (size_t)k + 1] : al + part[2 * (size_t)k + 1];
+        if (ctx->h_part_ptr[(size_t)k + 1] > ctx->h_part_ptr[(size_t)k]) {
+            h = have ? h + part[2 * (size_t)k] : part[2 * (size_t)k];
+            have = true;
+        }
+    }
+    carry[0] = h;
+    carry[1] = have ? 1.0 : 0.0;
+    carry[2] = al;
+}
+
+static void group_eval(cocoa_ctx* g, cocoa_eval_result* out);
+
+extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
+    CAPI_BEGIN(ctx)
+    require(out != nullptr, COCOA_E_ARG, "null out");
+    if (ctx->is_group()) {
+        group_eval(ctx, out);
+        return COCOA_OK;
+    }
+    eval_launch(ctx);
+    const EvalLocal ev = eval_collect(ctx);
+    double hinge = ev.hinge, alpha_sum = ev.alpha_sum;
+    const double w2 = ev.w2;
+    double counts[2] = {ev.err, ev.n_test};
     if (ctx->comm && ctx->comm->world > 1) {
         cocoa::Comm& cm = *ctx->comm;
         if (ctx->strict) {
-            // continue the partition-order merge of the previous ranks
-            // (OptUtils.scala:65-84 as Spark merges partitions, in index order):
-            // carry = {hinge, hinge-seen flag, alpha}
-            std::vector<double> part((size_t)2 * ctx->K_loc);
-            HIPCHK(hipMemcpyAsync(part.data(), ctx->eval_part.p, sizeof(double) * part.size(), hipMemcpyDeviceToHost,
-                                  ctx->stream));
-            HIPCHK(hipStreamSynchronize(ctx->stream));
             double carry[3] = {0.0, 0.0, 0.0};
             cm.chain_recv(carry, 3, false, ctx->stream);
-            bool have = carry[1] != 0.0;
-            double h = carry[0], al = carry[2];
-            for (int32_t k = 0; k < ctx->K_loc; ++k) {
-                al = (cm.rank == 0 && k == 0) ? part[2 * (size_t)k + 1] : al + part[2 * (size_t)k + 1];
-                if (ctx->h_part_ptr[(size_t)k + 1] > ctx->h_part_ptr[(size_t)k]) {
-                    h = have ? h + part[2 * (size_t)k] : part[2 * (size_t)k];
-                    have = true;
-                }
-            }
-            carry[0] = h;
-            carry[1] = have ? 1.0 : 0.0;
-            carry[2] = al;
+            strict_eval_carry(ctx, cm.rank == 0, carry);
             cm.chain_send(carry, 3, false, ctx->stream);
             cm.bcast_last(carry, 3, false, ctx->stream);
             hinge = carry[0];
@@ -1480,6 +1681,10 @@ extern "C" int cocoa_resume(cocoa_ctx* ctx, const cocoa_params* params, const co
 
 extern "C" int cocoa_sync(cocoa_ctx* ctx) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        for (cocoa_ctx* sub : ctx->subs) sub_check(cocoa_sync(sub), sub);
+        return COCOA_OK;
+    }
     HIPCHK(hipStreamSynchronize(ctx->stream));
     check_status(ctx);
     CAPI_END(ctx)
@@ -1487,6 +1692,11 @@ extern "C" int cocoa_sync(cocoa_ctx* ctx) {
 
 extern "C" int cocoa_get_w(cocoa_ctx* ctx, double* w_out) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        require(w_out != nullptr, COCOA_E_ARG, "cocoa_get_w: null output");
+        group_get_state(ctx, w_out, nullptr);
+        return COCOA_OK;
+    }
     require(ctx->inited && w_out, COCOA_E_STATE, "cocoa_get_w: not initialised");
     std::vector<double> dev((size_t)ctx->d);
     HIPCHK(hipMemcpyAsync(dev.data(), ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost, ctx->stream));
@@ -1498,6 +1708,11 @@ extern "C" int cocoa_get_w(cocoa_ctx* ctx, double* w_out) {
 
 extern "C" int cocoa_get_alpha(cocoa_ctx* ctx, double* alpha_out) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        require(alpha_out != nullptr, COCOA_E_ARG, "cocoa_get_alpha: null output");
+        group_get_state(ctx, nullptr, alpha_out);
+        return COCOA_OK;
+    }
     require(ctx->inited && alpha_out, COCOA_E_STATE, "cocoa_get_alpha: not initialised");
     if (ctx->tr.n)
         HIPCHK(hipMemcpyAsync(alpha_out, ctx->alpha.p, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyDeviceToHost,
@@ -1509,6 +1724,11 @@ extern "C" int cocoa_get_alpha(cocoa_ctx* ctx, double* alpha_out) {
 
 extern "C" int cocoa_set_w(cocoa_ctx* ctx, const double* w_in) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        require(w_in != nullptr, COCOA_E_ARG, "cocoa_set_w: null input");
+        group_set_state(ctx, w_in, nullptr);
+        return COCOA_OK;
+    }
     require(ctx->inited && w_in, COCOA_E_STATE, "cocoa_set_w: not initialised");
     std::vector<double> dev;
     ctx->to_device_order(w_in, dev);
@@ -1518,13 +1738,27 @@ extern "C" int cocoa_set_w(cocoa_ctx* ctx, const double* w_in) {
     CAPI_END(ctx)
 }
 
+// an alpha outside [0, 1] (or NaN) switches the fast solvers to the explicit
+// projected-gradient rule
+static bool any_outside_unit(const double* a, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+        if (!(a[i] >= 0.0 && a[i] <= 1.0)) return true;
+    return false;
+}
+
 extern "C" int cocoa_set_alpha(cocoa_ctx* ctx, const double* alpha_in) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        require(alpha_in != nullptr, COCOA_E_ARG, "cocoa_set_alpha: null input");
+        group_set_state(ctx, nullptr, alpha_in);
+        return COCOA_OK;
+    }
     require(ctx->inited && alpha_in, COCOA_E_STATE, "cocoa_set_alpha: not initialised");
     if (ctx->tr.n)
         HIPCHK(hipMemcpyAsync(ctx->alpha.p, alpha_in, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyHostToDevice,
                               ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->alpha_oob = ctx->alpha_oob || any_outside_unit(alpha_in, ctx->tr.n);
     CAPI_END(ctx)
 }
 
@@ -1580,12 +1814,19 @@ extern "C" int cocoa_checkpoint_save(cocoa_ctx* ctx, const char* path, int32_t t
     require(ctx->inited, COCOA_E_STATE, "cocoa_checkpoint_save: call cocoa_init first");
     require(path != nullptr && t >= 0, COCOA_E_ARG, "cocoa_checkpoint_save: bad argument");
     std::vector<double> w((size_t)ctx->d), dev((size_t)ctx->d), al((size_t)std::max<int64_t>(ctx->tr.n, 1));
-    HIPCHK(hipMemcpyAsync(dev.data(), ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost, ctx->stream));
-    if (ctx->tr.n)
-        HIPCHK(hipMemcpyAsync(al.data(), ctx->alpha.p, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyDeviceToHost,
+    if (ctx->is_group()) {
+        // the whole problem's state: the same file a one-device run writes
+        group_get_state(ctx, w.data(), al.data());  // (checks every device's solver status)
+    } else {
+        HIPCHK(hipMemcpyAsync(dev.data(), ctx->w.p, sizeof(double) * (size_t)ctx->d, hipMemcpyDeviceToHost,
                               ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    ctx->to_host_order(dev, w.data());
+        if (ctx->tr.n)
+            HIPCHK(hipMemcpyAsync(al.data(), ctx->alpha.p, sizeof(double) * (size_t)ctx->tr.n, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        check_status(ctx);  // never save (with a valid checksum) the state of an aborted solver launch
+        ctx->to_host_order(dev, w.data());
+    }
     const CkptHeader h = ckpt_header(ctx, t);
     uint64_t sum = 1469598103934665603ULL;
     sum = fnv1a(sum, &h, sizeof h);
@@ -1636,6 +1877,11 @@ extern "C" int cocoa_checkpoint_load(cocoa_ctx* ctx, const char* path, int32_t* 
     sum = fnv1a(sum, w.data(), sizeof(double) * w.size());
     sum = fnv1a(sum, al.data(), sizeof(double) * (size_t)ctx->tr.n);
     require(sum == stored, COCOA_E_IO, std::string("checkpoint checksum mismatch: ") + path);
+    if (ctx->is_group()) {
+        group_set_state(ctx, w.data(), al.data());
+        *t_out = h.t;
+        return COCOA_OK;
+    }
     std::vector<double> dev;
     ctx->to_device_order(w.data(), dev);
     HIPCHK(hipMemcpyAsync(ctx->w.p, dev.data(), sizeof(double) * (size_t)ctx->d, hipMemcpyHostToDevice, ctx->stream));
@@ -1644,6 +1890,7 @@ extern "C" int cocoa_checkpoint_load(cocoa_ctx* ctx, const char* path, int32_t* 
                               ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->xw_cached = false;
+    ctx->alpha_oob = ctx->alpha_oob || any_outside_unit(al.data(), ctx->tr.n);
     *t_out = h.t;
     CAPI_END(ctx)
 }
@@ -1653,12 +1900,22 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
                                 double* alpha, int32_t seed, int plus, double sigma, double* delta_w,
                                 double* delta_alpha) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {  // the device holding partition `part`
+        require(!ctx->g_k0.empty(), COCOA_E_STATE, "cocoa_local_sdca: no training data");
+        const int32_t r = group_owner_of_part(ctx, part);
+        cocoa_ctx* sub = ctx->subs[(size_t)r];
+        sub_check(cocoa_local_sdca(sub, part - ctx->g_k0[(size_t)r], w, local_iters, lambda, n, alpha, seed, plus,
+                                   sigma, delta_w, delta_alpha),
+                  sub);
+        return COCOA_OK;
+    }
     require(ctx->d > 0, COCOA_E_STATE, "cocoa_local_sdca: no training data");
     require(part >= 0 && part < ctx->K_loc && w && alpha && delta_w && local_iters >= 0, COCOA_E_ARG,
             "cocoa_local_sdca: bad argument");
     const int64_t p0 = ctx->h_part_ptr[(size_t)part], p1 = ctx->h_part_ptr[(size_t)part + 1];
     const int32_t nl = (int32_t)(p1 - p0);
     if (local_iters >= 1) require(nl >= 1, COCOA_E_ARG, "IllegalArgumentException: empty partition");
+    ensure_cols(ctx->tr, ctx->d, ctx->stream);
     const int64_t d = ctx->d;
     hipStream_t s = ctx->stream;
     // a one-partition problem over the loaded CSR
@@ -1733,6 +1990,13 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
 
 extern "C" int cocoa_samples(cocoa_ctx* ctx, int32_t part, int32_t seed_plus_t, int32_t count, int32_t* out) {
     CAPI_BEGIN(ctx)
+    if (ctx->is_group()) {
+        require(!ctx->g_k0.empty(), COCOA_E_STATE, "cocoa_samples: no training data");
+        const int32_t r = group_owner_of_part(ctx, part);
+        cocoa_ctx* sub = ctx->subs[(size_t)r];
+        sub_check(cocoa_samples(sub, part - ctx->g_k0[(size_t)r], seed_plus_t, count, out), sub);
+        return COCOA_OK;
+    }
     require(part >= 0 && part < ctx->K_loc && count >= 0 && out, COCOA_E_ARG, "cocoa_samples: bad argument");
     const int64_t h_pp[2] = {ctx->h_part_ptr[(size_t)part], ctx->h_part_ptr[(size_t)part + 1]};
     require(h_pp[1] > h_pp[0], COCOA_E_ARG, "IllegalArgumentException: empty partition");
@@ -1748,9 +2012,322 @@ extern "C" int cocoa_samples(cocoa_ctx* ctx, int32_t part, int32_t seed_plus_t, 
     CAPI_END(ctx)
 }
 
+// ------------------------------------------------ multi-device context --
+// cocoa_create_multi: ONE context over several GPUs, driven from the caller's
+// one thread, for a caller that runs the whole problem in one process (the
+// reference's single driver: hingeDriver.scala:84 -> CoCoA.runCoCoA, whose
+// reduce and `w +=` happen inside that call, CoCoA.scala:45-48).  Device r
+// holds the contiguous partition block [K r / N, K (r+1) / N) like rank r of
+// a multi-process run (same part_begin / num_parts_global, so sigma' = K gamma
+// and the scaling see the global K).  Per round every device runs its local
+// half on its own stream; the deltaW sums then meet on the devices' streams:
+//   fast   -- device 0 gathers the others' sums (peer copies over xGMI) and
+//             adds them in device order, every device copies the total;
+//   strict -- the ordered chain: device r's fold continues device r-1's (peer
+//             copy, then the fold kernel), the last device's total goes to all,
+// so strict stays bitwise equal to the single-device partition-order fold.
+// No host round trip inside a round.
+
+static void sub_check(int rc, const cocoa_ctx* sub) {
+    if (rc != COCOA_OK) throw Error(rc, sub ? sub->err : std::string(cocoa_last_error(nullptr)));
+}
+
+static int32_t group_owner_of_part(const cocoa_ctx* g, int32_t part) {
+    require(part >= 0 && part < g->K_loc, COCOA_E_ARG, "partition index out of range");
+    int32_t r = 0;
+    while (g->g_k0[(size_t)r + 1] <= part) ++r;
+    return r;
+}
+
+extern "C" int cocoa_create_multi(int32_t n_devices, const int32_t* devices, int strict, cocoa_ctx** out) {
+    if (!out) return COCOA_E_ARG;
+    *out = nullptr;
+    if (n_devices < 1 || n_devices > 64) {
+        cocoa_set_global_error("cocoa_create_multi: n_devices must be in [1, 64]");
+        return COCOA_E_ARG;
+    }
+    cocoa_ctx* g = new cocoa_ctx();
+    g->strict = strict != 0;
+    try {
+        for (int32_t r = 0; r < n_devices; ++r) {
+            const int dv = devices ? devices[r] : r;
+            cocoa_ctx* sub = nullptr;
+            const int rc = cocoa_create(dv, strict, nullptr, &sub);
+            if (rc) throw Error(rc, std::string("cocoa_create_multi: device ") + std::to_string(dv) + ": " +
+                                        cocoa_last_error(nullptr));
+            g->subs.push_back(sub);
+            HIPCHK(hipSetDevice(dv));
+            hipEvent_t e1 = nullptr, e2 = nullptr;
+            HIPCHK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+            g->g_ev.push_back(e1);
+            HIPCHK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+            g->g_ev_cp.push_back(e2);
+        }
+        g->device = g->subs[0]->device;
+        // peer access between distinct devices (xGMI); copies work without it too
+        for (cocoa_ctx* a : g->subs)
+            for (cocoa_ctx* b : g->subs) {
+                if (a->device == b->device) continue;
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, a->device, b->device) == hipSuccess && can) {
+                    HIPCHK(hipSetDevice(a->device));
+                    const hipError_t e = hipDeviceEnablePeerAccess(b->device, 0);
+                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+                    (void)hipGetLastError();
+                }
+            }
+        HIPCHK(hipSetDevice(g->device));
+    } catch (const Error& e) {
+        cocoa_set_global_error(e.what());
+        delete g;
+        return e.code;
+    }
+    *out = g;
+    return COCOA_OK;
+}
+
+extern "C" int cocoa_num_devices(cocoa_ctx* ctx, int32_t* n_devices, int32_t* devices, int32_t cap) {
+    CAPI_BEGIN(ctx)
+    require(n_devices != nullptr, COCOA_E_ARG, "cocoa_num_devices: null output");
+    *n_devices = ctx->is_group() ? (int32_t)ctx->subs.size() : 1;
+    for (int32_t r = 0; devices && r < cap && r < *n_devices; ++r)
+        devices[r] = ctx->is_group() ? ctx->subs[(size_t)r]->device : ctx->device;
+    CAPI_END(ctx)
+}
+
+// col == nullptr: dense rows (val = X[n][d])
+static void group_set_train(cocoa_ctx* g, int32_t K, const int64_t* part_ptr, const int64_t* row_ptr,
+                            const int32_t* col, const double* val, const double* y, int64_t n, int32_t d,
+                            int32_t part_begin, int32_t Kg) {
+    const int32_t N = (int32_t)g->subs.size();
+    const bool dense = col == nullptr;
+    require(part_begin == 0 && Kg == K, COCOA_E_ARG,
+            "a multi-device context holds the whole problem (part_begin = 0, num_parts_global = num_parts)");
+    require(K >= N, COCOA_E_ARG, "cocoa_set_train: fewer partitions than devices");
+    require(part_ptr && y && n >= 0 && d >= 1 && (dense || row_ptr), COCOA_E_ARG, "cocoa_set_train: bad argument");
+    require(part_ptr[0] == 0 && part_ptr[K] == n, COCOA_E_ARG, "part_ptr must span [0, n_rows]");
+    for (int32_t k = 0; k < K; ++k) require(part_ptr[k + 1] >= part_ptr[k], COCOA_E_ARG, "part_ptr not monotone");
+    if (!dense) require(row_ptr[0] == 0, COCOA_E_ARG, "row_ptr[0] must be 0");
+    g->g_k0.assign((size_t)N + 1, 0);
+    g->g_r0.assign((size_t)N + 1, 0);
+    for (int32_t r = 0; r <= N; ++r) {
+        g->g_k0[(size_t)r] = (int32_t)((int64_t)K * r / N);  // configs.shard_bounds
+        g->g_r0[(size_t)r] = part_ptr[g->g_k0[(size_t)r]];
+    }
+    // every device's host-side preparation (row norms, feature order, compact
+    // slices) and upload in parallel, one thread per device
+    std::vector<int> rcs((size_t)N, 0);
+    std::vector<std::thread> th;
+    for (int32_t r = 0; r < N; ++r)
+        th.emplace_back([&, r] {
+            cocoa_ctx* sub = g->subs[(size_t)r];
+            const int32_t k0 = g->g_k0[(size_t)r], k1 = g->g_k0[(size_t)r + 1];
+            const int64_t r0 = g->g_r0[(size_t)r], r1 = g->g_r0[(size_t)r + 1];
+            std::vector<int64_t> pp((size_t)(k1 - k0) + 1);
+            for (int32_t k = k0; k <= k1; ++k) pp[(size_t)(k - k0)] = part_ptr[k] - r0;
+            if (dense) {
+                rcs[(size_t)r] = cocoa_set_train_dense(sub, k1 - k0, pp.data(), val + r0 * (int64_t)d, y + r0, r1 - r0,
+                                                       d, k0, K);
+            } else {
+                const int64_t e0 = row_ptr[r0];
+                std::vector<int64_t> rp((size_t)(r1 - r0) + 1);
+                for (int64_t i = r0; i <= r1; ++i) rp[(size_t)(i - r0)] = row_ptr[i] - e0;
+                rcs[(size_t)r] = cocoa_set_train(sub, k1 - k0, pp.data(), rp.data(), col + e0, val + e0, y + r0,
+                                                 r1 - r0, d, k0, K);
+            }
+        });
+    for (auto& t : th) t.join();
+    for (int32_t r = 0; r < N; ++r) sub_check(rcs[(size_t)r], g->subs[(size_t)r]);
+    HIPCHK(hipSetDevice(g->device));
+    g->d = d;
+    g->K_loc = K;
+    g->K_glob = K;
+    g->part_begin = 0;
+    g->tr.n = n;
+    g->tr.nnz = dense ? n * (int64_t)d : row_ptr[n];
+    g->h_part_ptr.assign(part_ptr, part_ptr + K + 1);
+    g->tr_dense = g->subs[0]->tr_dense;
+    g->has_test = false;
+    g->te.n = 0;
+    g->inited = false;
+}
+
+static void group_set_test(cocoa_ctx* g, const int64_t* row_ptr, const int32_t* col, const double* val,
+                           const double* y, int64_t n_rows) {
+    const int32_t N = (int32_t)g->subs.size();
+    const bool dense = col == nullptr;
+    require(g->d > 0, COCOA_E_STATE, "cocoa_set_test: call cocoa_set_train first");
+    require(y && n_rows >= 0 && (dense || row_ptr), COCOA_E_ARG, "cocoa_set_test: bad argument");
+    if (!dense) require(row_ptr[0] == 0, COCOA_E_ARG, "row_ptr[0] must be 0");
+    g->g_t0.assign((size_t)N + 1, 0);
+    for (int32_t r = 0; r <= N; ++r) g->g_t0[(size_t)r] = n_rows * r / N;  // any row split (OptUtils.scala:95-98)
+    for (int32_t r = 0; r < N; ++r) {
+        cocoa_ctx* sub = g->subs[(size_t)r];
+        const int64_t t0 = g->g_t0[(size_t)r], t1 = g->g_t0[(size_t)r + 1];
+        if (dense) {
+            sub_check(cocoa_set_test_dense(sub, val + t0 * (int64_t)g->d, y + t0, t1 - t0), sub);
+        } else {
+            const int64_t e0 = row_ptr[t0];
+            std::vector<int64_t> rp((size_t)(t1 - t0) + 1);
+            for (int64_t i = t0; i <= t1; ++i) rp[(size_t)(i - t0)] = row_ptr[i] - e0;
+            sub_check(cocoa_set_test(sub, rp.data(), col + e0, val + e0, y + t0, t1 - t0), sub);
+        }
+    }
+    HIPCHK(hipSetDevice(g->device));
+    g->has_test = true;
+    g->te.n = n_rows;
+}
+
+static void group_init(cocoa_ctx* g, const cocoa_params* params, const cocoa_debug* debug, int method,
+                       const double* w_init) {
+    require(params && method >= 0 && method <= 4, COCOA_E_ARG, "cocoa_init: bad argument");
+    require(g->d > 0 && !g->g_k0.empty(), COCOA_E_STATE, "cocoa_init: no training data");
+    for (cocoa_ctx* sub : g->subs) sub_check(cocoa_init(sub, params, debug, method, w_init), sub);
+    HIPCHK(hipSetDevice(g->device));
+    g->P = *params;
+    g->D = debug ? *debug : cocoa_debug{10, 0, 100, 0};
+    g->method = method;
+    g->scaling = g->subs[0]->scaling;
+    g->alpha_oob = false;
+    const size_t N = g->subs.size();
+    if (!g->strict && N > 1) g->g_stage.alloc(sizeof(double) * (N - 1) * (size_t)g->d);
+    g->inited = true;
+}
+
+namespace {
+struct GroupPrev {
+    cocoa_ctx* prev;
+    hipEvent_t ev;
+};
+}  // namespace
+
+// strict chain: this device's fold continues the previous device's
+static void group_recv_prev(cocoa_ctx* c, void* user) {
+    const GroupPrev* p = (const GroupPrev*)user;
+    HIPCHK(hipStreamWaitEvent(c->stream, p->ev, 0));
+    HIPCHK(hipMemcpyPeerAsync(c->dw_sum, c->device, p->prev->dw_sum, p->prev->device, sizeof(double) * (size_t)c->d,
+                              c->stream));
+}
+
+static void group_round(cocoa_ctx* g, int32_t t) {
+    require(g->inited, COCOA_E_STATE, "cocoa_round: call cocoa_init first");
+    const size_t N = g->subs.size();
+    const size_t bytes = sizeof(double) * (size_t)g->d;
+    size_t owner = 0;  // the device whose dw_sum ends up holding the total
+    if (N == 1) {
+        HIPCHK(hipSetDevice(g->subs[0]->device));
+        run_local(g->subs[0], t, true);
+        return;
+    }
+    if (g->strict) {
+        for (size_t r = 0; r < N; ++r) {
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipSetDevice(sub->device));
+            if (r == 0) {
+                run_local(sub, t, false);
+            } else {
+                GroupPrev pv{g->subs[r - 1], g->g_ev[r - 1]};
+                run_local(sub, t, false, sub->dw_sum, group_recv_prev, &pv);
+            }
+            HIPCHK(hipEventRecord(g->g_ev[r], sub->stream));
+        }
+        owner = N - 1;
+    } else {
+        for (size_t r = 0; r < N; ++r) {
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipSetDevice(sub->device));
+            run_local(sub, t, false);
+            HIPCHK(hipEventRecord(g->g_ev[r], sub->stream));
+        }
+        // device 0: ((x_0 + x_1) + x_2) + ... in device order
+        cocoa_ctx* s0 = g->subs[0];
+        HIPCHK(hipSetDevice(s0->device));
+        double* stage = g->g_stage.as<double>();
+        for (size_t r = 1; r < N; ++r) {
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipStreamWaitEvent(s0->stream, g->g_ev[r], 0));
+            HIPCHK(hipMemcpyPeerAsync(stage + (r - 1) * (size_t)g->d, s0->device, sub->dw_sum, sub->device, bytes,
+                                      s0->stream));
+        }
+        s0->timed(COCOA_K_FOLD, [&] { launch_sum_into(s0->dw_sum, stage, (int32_t)(N - 1), g->d, s0->stream); });
+        HIPCHK(hipEventRecord(g->g_ev[0], s0->stream));
+        owner = 0;
+    }
+    cocoa_ctx* src = g->subs[owner];
+    for (size_t r = 0; r < N; ++r) {
+        cocoa_ctx* sub = g->subs[r];
+        HIPCHK(hipSetDevice(sub->device));
+        if (r != owner) {
+            HIPCHK(hipStreamWaitEvent(sub->stream, g->g_ev[owner], 0));
+            HIPCHK(hipMemcpyPeerAsync(sub->dw_sum, sub->device, src->dw_sum, src->device, bytes, sub->stream));
+            HIPCHK(hipEventRecord(g->g_ev_cp[r], sub->stream));
+        }
+        // w += sum * scaling (CoCoA.scala:48), identical on every device
+        sub->timed(COCOA_K_APPLY, [&] {
+            launch_apply(sub->w.as<double>(), sub->dw_sum, sub->d, sub->mult, sub->d_inv.as<int32_t>(), sub->stream);
+        });
+        sub->xw_cached = false;
+    }
+    // the owner's next fold overwrites its sum: only after every copy of it
+    HIPCHK(hipSetDevice(src->device));
+    for (size_t r = 0; r < N; ++r)
+        if (r != owner) HIPCHK(hipStreamWaitEvent(src->stream, g->g_ev_cp[r], 0));
+    HIPCHK(hipSetDevice(g->device));
+}
+
+static void group_eval(cocoa_ctx* g, cocoa_eval_result* out) {
+    require(g->inited, COCOA_E_STATE, "call cocoa_init first");
+    const size_t N = g->subs.size();
+    for (cocoa_ctx* sub : g->subs) {
+        HIPCHK(hipSetDevice(sub->device));
+        eval_launch(sub);
+    }
+    double hinge = 0.0, alpha_sum = 0.0, w2 = 0.0, err = 0.0, n_test = 0.0;
+    double carry[3] = {0.0, 0.0, 0.0};
+    for (size_t r = 0; r < N; ++r) {
+        cocoa_ctx* sub = g->subs[r];
+        HIPCHK(hipSetDevice(sub->device));
+        const EvalLocal ev = eval_collect(sub);
+        if (g->strict) {
+            strict_eval_carry(sub, r == 0, carry);  // the partition-order merge across devices
+        } else {
+            hinge = r == 0 ? ev.hinge : hinge + ev.hinge;  // device order
+            alpha_sum = r == 0 ? ev.alpha_sum : alpha_sum + ev.alpha_sum;
+        }
+        if (r == 0) w2 = ev.w2;
+        err += ev.err;  // integers: exact in any order
+        n_test += ev.n_test;
+    }
+    if (g->strict) {
+        hinge = carry[0];
+        alpha_sum = carry[2];
+    }
+    HIPCHK(hipSetDevice(g->device));
+    finish(g, hinge, alpha_sum, w2, (int64_t)err, (int64_t)n_test, out);
+}
+
+// (w in the original feature order, alpha of all rows) of a group
+static void group_get_state(cocoa_ctx* g, double* w, double* alpha) {
+    require(g->inited, COCOA_E_STATE, "not initialised");
+    if (w) sub_check(cocoa_get_w(g->subs[0], w), g->subs[0]);
+    for (size_t r = 0; alpha && r < g->subs.size(); ++r)
+        sub_check(cocoa_get_alpha(g->subs[r], alpha + g->g_r0[r]), g->subs[r]);
+    HIPCHK(hipSetDevice(g->device));
+}
+
+static void group_set_state(cocoa_ctx* g, const double* w, const double* alpha) {
+    require(g->inited, COCOA_E_STATE, "not initialised");
+    for (size_t r = 0; r < g->subs.size(); ++r) {
+        if (w) sub_check(cocoa_set_w(g->subs[r], w), g->subs[r]);
+        if (alpha) sub_check(cocoa_set_alpha(g->subs[r], alpha + g->g_r0[r]), g->subs[r]);
+    }
+    HIPCHK(hipSetDevice(g->device));
+}
+
 // ------------------------------------------------------------- profiling --
 extern "C" int cocoa_stats_enable(cocoa_ctx* ctx, int enable) {
     CAPI_BEGIN(ctx)
+    for (cocoa_ctx* sub : ctx->subs) sub_check(cocoa_stats_enable(sub, enable), sub);
     ctx->drain();
     ctx->stats = enable != 0;
     CAPI_END(ctx)
@@ -1759,6 +2336,20 @@ extern "C" int cocoa_stats_enable(cocoa_ctx* ctx, int enable) {
 extern "C" int cocoa_kernel_stats(cocoa_ctx* ctx, int kernel, double* total_ms, int64_t* launches) {
     CAPI_BEGIN(ctx)
     require(kernel >= 0 && kernel < COCOA_K_COUNT, COCOA_E_ARG, "bad kernel id");
+    if (ctx->is_group()) {  // summed over the devices
+        double tot = 0.0;
+        int64_t cnt = 0;
+        for (cocoa_ctx* sub : ctx->subs) {
+            double m = 0.0;
+            int64_t c = 0;
+            sub_check(cocoa_kernel_stats(sub, kernel, &m, &c), sub);
+            tot += m;
+            cnt += c;
+        }
+        if (total_ms) *total_ms = tot;
+        if (launches) *launches = cnt;
+        return COCOA_OK;
+    }
     ctx->drain();
     if (total_ms) *total_ms = ctx->tot_ms[kernel];
     if (launches) *launches = ctx->cnt[kernel];
@@ -1767,6 +2358,7 @@ extern "C" int cocoa_kernel_stats(cocoa_ctx* ctx, int kernel, double* total_ms, 
 
 extern "C" int cocoa_stats_reset(cocoa_ctx* ctx) {
     CAPI_BEGIN(ctx)
+    for (cocoa_ctx* sub : ctx->subs) sub_check(cocoa_stats_reset(sub), sub);
     ctx->drain();
     for (int i = 0; i < COCOA_K_COUNT; ++i) ctx->tot_ms[i] = 0, ctx->cnt[i] = 0;
     CAPI_END(ctx)
@@ -1774,6 +2366,7 @@ extern "C" int cocoa_stats_reset(cocoa_ctx* ctx) {
 
 extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
     CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_solver_profile");
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     if (enable) {
         ctx->prof.alloc_zero(sizeof(uint64_t) * ((size_t)ctx->K_loc * 32 + 8), ctx->stream);  // + gram_kernel phases
@@ -1786,6 +2379,7 @@ extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
 
 extern "C" int cocoa_solver_profile_read(cocoa_ctx* ctx, uint64_t* out, int64_t count) {
     CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_solver_profile_read");
     require(out && ctx->prof.p, COCOA_E_STATE, "solver profiling not enabled");
     const size_t n = std::min<size_t>((size_t)count, (size_t)ctx->K_loc * 32 + 8);
     HIPCHK(hipMemcpyAsync(out, ctx->prof.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
@@ -1796,6 +2390,15 @@ extern "C" int cocoa_solver_profile_read(cocoa_ctx* ctx, uint64_t* out, int64_t 
 extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
     CAPI_BEGIN(ctx)
     require(buf && len > 0, COCOA_E_ARG, "bad buffer");
+    if (ctx->is_group()) {  // device 0's plan (every device plans alike) + the device count
+        sub_check(cocoa_plan_info(ctx->subs[0], buf, len), ctx->subs[0]);
+        std::string p(buf);
+        if (!p.empty() && p.back() == '}') p.pop_back();
+        p += ",\"n_devices\":" + std::to_string(ctx->subs.size()) + "}";
+        require((int)p.size() < len, COCOA_E_ARG, "cocoa_plan_info: buffer too small");
+        std::memcpy(buf, p.c_str(), p.size() + 1);
+        return COCOA_OK;
+    }
     std::snprintf(buf, (size_t)len,
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"

@@ -136,7 +136,7 @@ struct GramSolverArgs {
     int32_t raw_alpha;
     int32_t hot;              // columns [0, hot) of deltaW live in LDS (set by launch_solver_gram)
     int32_t diag;             // diagnostics only (COCOA_GRAM_DIAG): 1 skip scatter atomics, 2 skip gathers
-    int32_t pad2;
+    int32_t proj;             // 1: alpha may lie outside [0, 1] -- explicit projected-gradient skip (CoCoA.scala:166-172)
     double lam_n, inv_lam_n;
     double sigma;             // sigma' = K gamma (CoCoA+)
     double scaling;
@@ -154,7 +154,8 @@ struct DenseArgs {
     double* dw;               // K_loc * d private deltaW (every entry written)
     const double* w;
     int64_t d;
-    int32_t H, pad;
+    int32_t H;
+    int32_t proj;             // 1: alpha may lie outside [0, 1] -- explicit projected-gradient skip (CoCoA.scala:166-172)
     double lam_n, inv_lam_n;
     double sigma;             // sigma' = K gamma (CoCoA+)
     double scaling;
@@ -226,6 +227,8 @@ void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H,
 // inv (device order -> original feature index) places the unapplied sum in the
 // original order, the order ranks exchange it in
 void launch_zero(double* p, int64_t n, int blocks, hipStream_t s);
+void launch_dense_cols(int32_t* col, uint16_t* col16, int64_t nnz, int32_t d, hipStream_t s);
+void launch_sum_into(double* dst, const double* stage, int32_t m, int64_t d, hipStream_t s);
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
                  const int32_t* inv, bool zero, hipStream_t s, const double* init = nullptr);
 // compact deltaW slices: column j's sum is the gather of dw[fpos[fptr[j] ..

@@ -41,11 +41,16 @@ void launch_gram(const GramArgs& a, hipStream_t s) {
     if (grid > 0) gram_kernel<<<(unsigned)grid, kGramThreads, sizeof(GramLds), s>>>(a);
 }
 
+template <int MODE, bool HOTLDS, bool PROJ>
+static void launch_sg3(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
+    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    solver_gram_kernel<MODE, HOTLDS, PROJ><<<grid, kGThreads, lds, s>>>(a);
+}
 template <int MODE, bool HOTLDS>
 static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
-    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    solver_gram_kernel<MODE, HOTLDS><<<grid, kGThreads, lds, s>>>(a);
+    if (a.proj) launch_sg3<MODE, HOTLDS, true>(a, grid, lds, s);
+    else launch_sg3<MODE, HOTLDS, false>(a, grid, lds, s);
 }
 
 // deltaW columns in LDS (HOTLDS) or all in the L2-resident slice.  The memory
@@ -79,9 +84,11 @@ void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t
         else launch_sg<MODE_MBCD, false>(g, grid, lds, s);
         return;
     }
+#ifdef COCOA_DIAG
     if (mode == MODE_PLUS) launch_sg<MODE_PLUS, true>(g, grid, lds, s);
     else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, true>(g, grid, lds, s);
     else launch_sg<MODE_MBCD, true>(g, grid, lds, s);
+#endif
 }
 
 // ----------------------------------------------------------- fused eval --
@@ -275,11 +282,16 @@ bool dense_solver_fits(int64_t d, int64_t max_nl) {
 }
 bool dense_eval_fits(int64_t d) { return d >= 2 && (d & 1) == 0 && d <= 4096; }
 
+template <int MODE, int CPT, int P, bool PROJ>
+static void launch_ds3(const DenseArgs& a, int grid, size_t lds, hipStream_t s) {
+    (void)hipFuncSetAttribute((const void*)dense_solver_kernel<MODE, CPT, P, kDT, PROJ>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dense_solver_kernel<MODE, CPT, P, kDT, PROJ><<<grid, kDT, lds, s>>>(a);
+}
 template <int MODE, int CPT, int P>
 static void launch_ds(const DenseArgs& a, int grid, size_t lds, hipStream_t s) {
-    (void)hipFuncSetAttribute((const void*)dense_solver_kernel<MODE, CPT, P, kDT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dense_solver_kernel<MODE, CPT, P, kDT><<<grid, kDT, lds, s>>>(a);
+    if (a.proj) launch_ds3<MODE, CPT, P, true>(a, grid, lds, s);
+    else launch_ds3<MODE, CPT, P, false>(a, grid, lds, s);
 }
 
 template <int MODE>

@@ -163,6 +163,36 @@ void launch_zero(double* p, int64_t n, int blocks, hipStream_t s) {
     if (n >= 2) zero_kernel<<<blocks < 1 ? 1 : blocks, 256, 0, s>>>(p, n / 2);
 }
 
+// column indices of dense rows (entry q of row-major X[n][d] is column q mod d),
+// built on the device only when a CSR kernel needs them (strict mode, the
+// chain / SGD solvers): cocoa_set_train_dense keeps no column array
+__global__ __launch_bounds__(256) void dense_cols_kernel(int32_t* col, uint16_t* col16, int64_t nnz, int32_t d) {
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nnz; q += (int64_t)gridDim.x * 256) {
+        const int32_t c = (int32_t)(q % d);
+        col[q] = c;
+        if (col16) col16[q] = (uint16_t)c;
+    }
+}
+
+// dst[j] = ((dst[j] + stage[0][j]) + stage[1][j]) + ... : the multi-device
+// context's fast exchange, the other devices' sums added in device order
+__global__ __launch_bounds__(256) void sum_into_kernel(double* dst, const double* stage, int32_t m, int64_t d) {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < d; j += (int64_t)gridDim.x * 256) {
+        double acc = dst[j];
+        for (int32_t r = 0; r < m; ++r) acc = acc + stage[(size_t)r * (size_t)d + (size_t)j];
+        dst[j] = acc;
+    }
+}
+
+void launch_sum_into(double* dst, const double* stage, int32_t m, int64_t d, hipStream_t s) {
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((d + 255) / 256, 2048));
+    if (m > 0 && d > 0) sum_into_kernel<<<blocks, 256, 0, s>>>(dst, stage, m, d);
+}
+
+void launch_dense_cols(int32_t* col, uint16_t* col16, int64_t nnz, int32_t d, hipStream_t s) {
+    if (nnz > 0) dense_cols_kernel<<<2048, 256, 0, s>>>(col, col16, nnz, d);
+}
+
 __global__ __launch_bounds__(256) void apply_kernel(double* w, const double* dw_sum, int64_t d, double mult,
                                                     const int32_t* inv) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x)

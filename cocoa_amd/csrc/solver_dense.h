@@ -42,7 +42,7 @@ constexpr int kDT = 256;
 __device__ __forceinline__ f64x2v ld_nt2(const double* p) { return __builtin_nontemporal_load((const f64x2v*)p); }
 
 
-template <int MODE, int CPT, int P, int NTH>
+template <int MODE, int CPT, int P, int NTH, bool PROJ>
 __global__ __launch_bounds__(NTH) void dense_solver_kernel(DenseArgs a) {
     constexpr int NWV = NTH / 64;
     extern __shared__ double al[];  // alpha of the partition (rows [p0, p0 + nl))
@@ -124,9 +124,14 @@ __global__ __launch_bounds__(NTH) void dense_solver_kernel(DenseArgs a) {
                 for (int i = 1; i < NWV; ++i) tot += red[s & 1][i];
                 const double yv = readlane_d(y0, j), rq = readlane_d(rq0, j);
                 const double grad = (yv * tot - 1.0) * a.lam_n;  // CoCoA.scala:157-163
-                // projection + skip (CoCoA.scala:166-172) fold into the clamp: a
-                // vanishing projected gradient returns aa, so c = 0
-                const double nt = rq < 0.0 ? 1.0 : fmin(fmax(aa - grad * rq, 0.0), 1.0);
+                // projection + skip (CoCoA.scala:166-172) fold into the clamp while aa
+                // lies in [0, 1]: a vanishing projected gradient returns aa, so c = 0.
+                // PROJ (alpha possibly outside [0, 1]): the explicit skip test.
+                double nt = rq < 0.0 ? 1.0 : fmin(fmax(aa - grad * rq, 0.0), 1.0);
+                if (PROJ) {
+                    const double pg = aa <= 0.0 ? fmin(grad, 0.0) : (aa >= 1.0 ? fmax(grad, 0.0) : grad);
+                    if (pg == 0.0) nt = aa;
+                }
                 const double cc = yv * (nt - aa) * a.inv_lam_n;  // CoCoA.scala:181
                 if (lane == 0) al[r] = nt;
 #pragma unroll

@@ -367,10 +367,15 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
 //     nt   = clamp(aa - grad / qii, 0, 1)
 //          = clamp(AE - B sdot)     B = A / qii, E = Kx / qii, AE = aa - E
 //     c    = y (nt - aa) / (lambda n) = Y nt - YA,   YA = Y aa
-// and nt is the new alpha whether or not the projected gradient vanishes:
-// with aa = 0 and grad >= 0, or aa = 1 and grad <= 0, the clamp returns aa.
-// An empty row (qii = 0) always gets alpha = 1 (grad = -lambda n < 0):
-// B = 0, E = -1.  MbCD (MinibatchCD.scala:104): A = 0, so B = 0.
+// and, while aa lies in [0, 1], nt is the new alpha whether or not the
+// projected gradient vanishes: with aa = 0 and grad >= 0, or aa = 1 and
+// grad <= 0, the clamp returns aa.  An alpha outside [0, 1] (scaling > 1 --
+// CoCoA+ gamma > 1, CoCoA beta > K -- or an alpha set from outside) needs the
+// explicit test of CoCoA.scala:166-172: with u = AE - B sdot = aa - grad/qii,
+// the step is skipped (nt = aa) when aa <= 0 and u <= aa or aa >= 1 and
+// u >= aa; that is the PROJ variant of the kernel.  An empty row (qii = 0) has
+// grad = -lambda n < 0 and gets alpha = 1 unless skipped: B = 0 and E = -1e300,
+// so u is huge for any aa.  MbCD (MinibatchCD.scala:104): A = 0, so B = 0.
 constexpr int kGWin = kGSlots + kGB;     // loader's look-back for alpha forwarding: 5 batches
 constexpr int kGE = 8192;                // staged entries (LDS ring positions)
 constexpr int kGUnitB = 64 * 13;         // bytes of one 64-entry ring unit
@@ -383,11 +388,13 @@ constexpr int kGGt = 4;                  // Gram-row ring (batches)
 struct GRec {                          // one step (64 B)
     double B, Y, AE, YA;               // AE, YA: set by the chain (its alpha prefetch or a forward)
     double E;
+    double AA;                         // alpha before the step (PROJ: the projected-gradient skip test)
     int32_t r;                         // sampled row (partition-local); padding steps: the alpha sink
     int32_t fw;                        // ring position (mod 128) of the next step with the same row, -1
     int32_t fwd;                       // AE / YA already forwarded (the prefetched alpha is stale)
-    int32_t pad[3];
+    int32_t pad;
 };
+static_assert(sizeof(GRec) == 64, "GRec layout");
 
 struct GLay {                          // one batch's rows, for the fetch and memory waves
     int64_t sb[kGB];                   // row starts in the CSR
@@ -430,7 +437,7 @@ __device__ __forceinline__ void gram_row_consts(const GramSolverArgs& a, double 
         E = Kx * rq;
     } else {
         B = 0.0;
-        E = -1.0;
+        E = -1e300;  // u = aa - E: the clamp gives 1 for every aa (and PROJ skips aa >= 1)
     }
     Y = y * a.inv_lam_n;
 }
@@ -475,7 +482,17 @@ __device__ __forceinline__ void ring_get(const GramSolverLds& S, int32_t us, int
 //                          marks) and row layouts, up to kGRing batches ahead;
 //   waves 3..    fetch  -- copy each batch's (column, value) entries into the
 //                          LDS ring (LDS DMA), ahead of the gathers.
-template <int MODE, bool HOTLDS>
+// CoCoA.scala:166-178 on u = aa - grad / qii: the clamp, and with PROJ the
+// projected-gradient skip for an alpha outside [0, 1]
+template <bool PROJ>
+__device__ __forceinline__ double gram_rule(double u, double aa) {
+    const double nt = fmin(fmax(u, 0.0), 1.0);
+    if (!PROJ) return nt;
+    const bool skip = (aa <= 0.0 && u <= aa) || (aa >= 1.0 && u >= aa);
+    return skip ? aa : nt;
+}
+
+template <int MODE, bool HOTLDS, bool PROJ>
 __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramSolverLds& S = *(GramSolverLds*)lds_raw;
@@ -827,6 +844,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             const double aa = alv[R.r];
             R.AE = aa - R.E;
             R.YA = R.Y * aa;
+            if (PROJ) R.AA = aa;
         }
         wave_lds_sync();
         // One batch.  Alpha of batch g+4 is loaded at the start of batch g (rows met
@@ -858,7 +876,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             // this batch's records in the lanes of its quarter (lane slot0 + i holds step
             // i, next to its accumulator): every step evaluates the update rule on all
             // lanes at once and broadcasts one coefficient
-            double rB = 0.0, rY = 0.0, rAE = 0.0, rYA = 0.0, rE = 0.0;
+            double rB = 0.0, rY = 0.0, rAE = 0.0, rYA = 0.0, rE = 0.0, rAA = 0.5;
             int32_t rR = nl, rF = -1;
             if (mine) {
                 const GRec& R = S.rec[(g % kGRing) * kGB + (lane & (kGB - 1))];
@@ -867,6 +885,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 rAE = R.AE;
                 rYA = R.YA;
                 rE = R.E;
+                if (PROJ) rAA = R.AA;
                 rR = R.r;
                 rF = R.fw;
             }
@@ -880,7 +899,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 #pragma unroll
             for (int i = 0; i < kGB; ++i) {
                 // CoCoA.scala:159-186 / MinibatchCD.scala:104-123 (see above)
-                const double nt = fmin(fmax(fma(-rB, acc, rAE), 0.0), 1.0);
+                const double nt = gram_rule<PROJ>(fma(-rB, acc, rAE), rAA);
                 if (MODE != MODE_MBCD) {
                     const double cf = readlane_d(fma(rY, nt, -rYA), slot0 + i);
                     acc = fma(cf, gcur[i], acc);
@@ -894,6 +913,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         if (lane == slot0 + (sp - g * kGB)) {  // this batch: its lane's registers
                             rAE = nts - rE;
                             rYA = rY * nts;
+                            if (PROJ) rAA = nts;
                         }
                         if (lane == slot0 + i) rR = nl;  // the later step stores the row's alpha
                     } else {
@@ -901,12 +921,13 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         const double tE = T.E, tY = T.Y;
                         T.AE = nts - tE;
                         T.YA = tY * nts;
+                        if (PROJ) T.AA = nts;
                         T.fwd = 1;
                     }
                 }
             }
             {
-                const double nt = fmin(fmax(fma(-rB, acc, rAE), 0.0), 1.0);
+                const double nt = gram_rule<PROJ>(fma(-rB, acc, rAE), rAA);
                 const double cf = fma(rY, nt, -rYA);
                 if (mine) {
                     alv[rR] = nt;
@@ -925,6 +946,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 if (!R3.fwd) {
                     R3.AE = afill - R3.E;
                     R3.YA = R3.Y * afill;
+                    if (PROJ) R3.AA = afill;
                 }
             }
             wave_lds_sync();

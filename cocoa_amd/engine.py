@@ -49,15 +49,37 @@ class Comm:
             pass
 
 
+def _dense_rows(data, chunk=1 << 14):
+    """Rows that store every feature 0..d-1 in index order (epsilon-shaped, C3):
+    the value array is then the row-major matrix itself."""
+    n, d = data.n, data.num_features
+    if n < 1 or len(data.col) != n * d:
+        return False
+    if not np.array_equal(data.row_ptr, np.arange(n + 1, dtype=np.int64) * d):
+        return False
+    cols = data.col.reshape(n, d)
+    ar = np.arange(d, dtype=np.int32)
+    return all(np.array_equal(cols[r:r + chunk], np.broadcast_to(ar, (min(chunk, n - r), d)))
+               for r in range(0, n, chunk))
+
+
 class Engine:
-    def __init__(self, device=0, strict=False, stream=None):
+    def __init__(self, device=0, strict=False, stream=None, devices=None):
         """stream: a hipStream_t handle as int (e.g. torch.cuda.current_stream().cuda_stream).
+        devices: a list of device ordinals -> ONE context over all of them
+        (cocoa_create_multi): the partitions are split over the devices and
+        every round / eval exchanges between them internally.
 
         A process that also uses torch on the GPU must initialise torch's HIP
         runtime (torch ships its own libamdhip64) before the first Engine opens
         the device, e.g. `import torch; torch.cuda.init()` first."""
         h = ctypes.c_void_p()
-        C.check(C.lib().cocoa_create(int(device), 1 if strict else 0, ctypes.c_void_p(stream or 0), ctypes.byref(h)))
+        if devices is not None:
+            devs = np.ascontiguousarray(devices, np.int32)
+            C.check(C.lib().cocoa_create_multi(len(devs), C.i32p(devs), 1 if strict else 0, ctypes.byref(h)))
+        else:
+            C.check(C.lib().cocoa_create(int(device), 1 if strict else 0, ctypes.c_void_p(stream or 0),
+                                         ctypes.byref(h)))
         self.h = h
         self.strict = strict
         self.d = 0
@@ -69,6 +91,9 @@ class Engine:
         data = data.contiguous()
         K = data.num_parts
         Kg = K if num_parts_global is None else num_parts_global
+        if _dense_rows(data):  # no column array crosses the ABI (cocoa_set_train_dense)
+            self.set_train_dense(data.val.reshape(data.n, data.num_features), data.y, data.part_ptr, part_begin, Kg)
+            return
         C.check(C.lib().cocoa_set_train(self.h, K, C.i64p(data.part_ptr), C.i64p(data.row_ptr), C.i32p(data.col),
                                         C.f64p(data.val), C.f64p(data.y), data.n, data.num_features, part_begin, Kg),
                 self.h)
@@ -78,6 +103,9 @@ class Engine:
 
     def set_test(self, data):
         data = data.contiguous()
+        if self.d and data.num_features == self.d and _dense_rows(data):
+            self.set_test_dense(data.val.reshape(data.n, data.num_features), data.y)
+            return
         C.check(C.lib().cocoa_set_test(self.h, C.i64p(data.row_ptr), C.i32p(data.col), C.f64p(data.val),
                                        C.f64p(data.y), data.n), self.h)
 
@@ -104,6 +132,13 @@ class Engine:
         """Attach a communicator (cocoa_comm_init): round / eval / run then
         exchange deltaW and the objective sums between the ranks internally."""
         C.check(C.lib().cocoa_comm_init(self.h, C.TRANSPORTS[transport], rank, world, uid), self.h)
+
+    def devices(self):
+        """Device ordinals of this context (one for cocoa_create)."""
+        n = ctypes.c_int32()
+        buf = np.zeros(64, np.int32)
+        C.check(C.lib().cocoa_num_devices(self.h, ctypes.byref(n), C.i32p(buf), len(buf)), self.h)
+        return [int(x) for x in buf[:n.value]]
 
     def comm_info(self):
         t, r, w = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define COCOA_CAPI_VERSION 2
+#define COCOA_CAPI_VERSION 3
 
 /* error codes */
 #define COCOA_OK 0
@@ -93,6 +93,25 @@ typedef struct cocoa_ctx cocoa_ctx;
  * restatement), 0 = fast mode (wave-tree dots, FMA; agrees within 1e-9).
  * stream: a hipStream_t to run on (NULL = a stream owned by the context). */
 int cocoa_create(int device, int strict, void *stream, cocoa_ctx **out);
+/* ONE context over n_devices GPUs (devices: their ordinals, NULL = 0..n-1;
+ * an ordinal may repeat), driven from the caller's one thread -- the shape of
+ * the reference's single driver process (hingeDriver.scala:84 ->
+ * CoCoA.runCoCoA, whose deltaW reduce and `w +=` happen inside the call,
+ * CoCoA.scala:45-48; SURVEY.md 8(b) `cocoa_create(n_gpus, ...)`).  Device r
+ * holds the contiguous partition block [K r / n, K (r+1) / n) of
+ * cocoa_set_train's data (which must be the whole problem: part_begin 0,
+ * num_parts_global = num_parts) and the test rows [n_t r / n, n_t (r+1) / n).
+ * Every round the devices exchange deltaW on their own streams (peer copies over
+ * xGMI; fast: an ordered sum on device 0, strict: the partition-order chain,
+ * so strict results stay bitwise equal to one device); cocoa_eval merges the
+ * objective terms; w / alpha / checkpoints are those of the whole problem (a
+ * checkpoint is interchangeable with a one-device context's).  The
+ * caller-driven exchange entry points (cocoa_round_local, cocoa_round_apply,
+ * cocoa_dw_sum_device_ptr, cocoa_set_dw_sum_buffer, cocoa_comm_init) and the
+ * solver-profile diagnostics return COCOA_E_STATE on such a context. */
+int cocoa_create_multi(int32_t n_devices, const int32_t *devices, int strict, cocoa_ctx **out);
+/* Devices of a context: n_devices (1 for cocoa_create), their ordinals into devices[cap]. */
+int cocoa_num_devices(cocoa_ctx *ctx, int32_t *n_devices, int32_t *devices, int32_t cap);
 int cocoa_destroy(cocoa_ctx *ctx);
 const char *cocoa_last_error(const cocoa_ctx *ctx);
 int cocoa_version(void);
@@ -111,6 +130,7 @@ int cocoa_version(void);
  * the single-process reference order. */
 #define COCOA_TRANSPORT_RCCL 0
 #define COCOA_TRANSPORT_HOST 1
+#define COCOA_TRANSPORT_LOCAL 2 /* reported by cocoa_comm_info for a multi-device context (not for cocoa_comm_*) */
 #define COCOA_COMM_UID_BYTES 128
 typedef struct cocoa_comm cocoa_comm;
 /* Made once, on rank 0 (HOST: opens rank 0's listening socket in this process). */

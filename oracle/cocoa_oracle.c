@@ -453,21 +453,89 @@ static void sgd_local(const int64_t *row_ptr, const int32_t *col, const double *
 /* ------------------------------------------------------------------------- */
 /* sum of hinge losses: per-partition reduceLeft in row order, partitions
  * merged in index order (Spark RDD.reduce). */
-static double hinge_sum(const oracle_data *D, const double *w) {
+/* Partition-parallel evaluation, as the reference's evaluation is a Spark job
+ * over the partitions (local[N]: one task per partition, N at a time): every
+ * partition folds its own rows, the driver merges the partition results in
+ * partition order -- so the result does not depend on the thread count. */
+typedef struct {
+    const oracle_data *D;
+    const double *w;
+    double *part;      /* per-partition hinge fold */
+    int64_t *cnt;      /* per-partition error count */
+    int nt, tid;
+} eval_arg;
+
+static double hinge_part(const oracle_data *D, const double *w, int32_t k) {
+    int64_t r0 = D->part_ptr[k], r1 = D->part_ptr[k + 1];
+    double acc = 0.0;
+    for (int64_t r = r0; r < r1; ++r) {
+        int64_t b = D->row_ptr[r], z = D->row_ptr[r + 1] - b;
+        double h = jmax(1.0 - D->y[r] * (sp_dot(D->col + b, D->val + b, z, w)), 0.0); /* :57-61 */
+        acc = (r == r0) ? h : acc + h;                                /* reduceLeft */
+    }
+    return acc;
+}
+
+static int64_t errors_rows(const oracle_data *D, const double *w, int64_t r0, int64_t r1) {
+    int64_t cnt = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+        int64_t b = D->row_ptr[r], z = D->row_ptr[r + 1] - b;
+        if (!((sp_dot(D->col + b, D->val + b, z, w)) * (D->y[r]) > 0)) ++cnt; /* OptUtils.scala:97 */
+    }
+    return cnt;
+}
+
+static void *eval_worker(void *p) {
+    eval_arg *a = (eval_arg *)p;
+    if (a->part)
+        for (int32_t k = a->tid; k < a->D->K; k += a->nt) a->part[k] = hinge_part(a->D, a->w, k);
+    if (a->cnt)  /* integer counts: any split of the rows gives the same total */
+        a->cnt[a->tid] = errors_rows(a->D, a->w, a->D->n * a->tid / a->nt, a->D->n * (a->tid + 1) / a->nt);
+    return NULL;
+}
+
+/* per-partition hinge folds (part) or per-thread error counts (cnt[thread]) */
+static void eval_parts(const oracle_data *D, const double *w, double *part, int64_t *cnt, int nthreads) {
+    int nt = part ? (nthreads < D->K ? nthreads : D->K) : nthreads;
+    if (nt > 256) nt = 256;
+    if (nt <= 1) {
+        eval_arg a = {D, w, part, cnt, 1, 0};
+        eval_worker(&a);
+        return;
+    }
+    pthread_t th[256];
+    eval_arg args[256];
+    for (int i = 0; i < nt; ++i) {
+        eval_arg a = {D, w, part, cnt, nt, i};
+        args[i] = a;
+        pthread_create(&th[i], NULL, eval_worker, &args[i]);
+    }
+    for (int i = 0; i < nt; ++i) pthread_join(th[i], NULL);
+}
+
+static double hinge_sum_mt(const oracle_data *D, const double *w, int nthreads) {
+    double *part = (double *)malloc(sizeof(double) * ((size_t)D->K + 1));
+    eval_parts(D, w, part, NULL, nthreads);
     double tot = 0.0;
     int have = 0;
-    for (int32_t k = 0; k < D->K; ++k) {
-        int64_t r0 = D->part_ptr[k], r1 = D->part_ptr[k + 1];
-        if (r1 <= r0) continue;
-        double acc = 0.0;
-        for (int64_t r = r0; r < r1; ++r) {
-            int64_t b = D->row_ptr[r], z = D->row_ptr[r + 1] - b;
-            double h = jmax(1.0 - D->y[r] * (sp_dot(D->col + b, D->val + b, z, w)), 0.0); /* :57-61 */
-            acc = (r == r0) ? h : acc + h;                            /* reduceLeft */
-        }
-        tot = have ? tot + acc : acc;
+    for (int32_t k = 0; k < D->K; ++k) {                             /* merge in partition order */
+        if (D->part_ptr[k + 1] <= D->part_ptr[k]) continue;
+        tot = have ? tot + part[k] : part[k];
         have = 1;
     }
+    free(part);
+    return tot;
+}
+
+static double hinge_sum(const oracle_data *D, const double *w) { return hinge_sum_mt(D, w, 1); }
+
+static int64_t error_count_mt(const oracle_data *D, const double *w, int nthreads) {
+    int nt = nthreads < 1 ? 1 : (nthreads > 256 ? 256 : nthreads);
+    int64_t *cnt = (int64_t *)calloc((size_t)nt, sizeof(int64_t));
+    eval_parts(D, w, NULL, cnt, nt);
+    int64_t tot = 0;
+    for (int i = 0; i < nt; ++i) tot += cnt[i];
+    free(cnt);
     return tot;
 }
 
@@ -502,14 +570,7 @@ double oracle_gap(const oracle_data *D, const double *w, const double *alpha, do
 }
 
 /* returns the error COUNT; the reference divides by n (OptUtils.scala:95-98) */
-int64_t oracle_error_count(const oracle_data *D, const double *w) {
-    int64_t cnt = 0;
-    for (int64_t r = 0; r < D->n; ++r) {
-        int64_t b = D->row_ptr[r], z = D->row_ptr[r + 1] - b;
-        if (!((sp_dot(D->col + b, D->val + b, z, w)) * (D->y[r]) > 0)) ++cnt;
-    }
-    return cnt;
-}
+int64_t oracle_error_count(const oracle_data *D, const double *w) { return error_count_mt(D, w, 1); }
 
 /* ------------------------------------------------------------------------- */
 /* Round drivers: CoCoA.runCoCoA (CoCoA.scala:22-66), MinibatchCD.runMbCD      */
@@ -699,13 +760,13 @@ void oracle_run_round(oracle_run *R, int32_t t) {
  * problem the objectives are that share's terms over the global n. */
 void oracle_run_eval(const oracle_run *R, const oracle_data *test, double *out) {
     const double n = (double)R->n;
-    const double h = hinge_sum(&R->D, R->w);
+    const double h = hinge_sum_mt(&R->D, R->w, R->nthreads);
     const double a = alpha_sum_parts(&R->D, R->alpha);
     const double nw = dense_norm2(R->w, R->D.d);
     out[0] = h / n + (0.5 * R->lambda * (nw * nw));                  /* :73-75 */
     out[1] = (-R->lambda / 2 * (nw * nw)) + (a / n);                  /* :80-84 */
     out[2] = out[0] - out[1];                                         /* :89-91 */
-    out[3] = test ? (double)oracle_error_count(test, R->w) : -1.0;
+    out[3] = test ? (double)error_count_mt(test, R->w, R->nthreads) : -1.0;
     out[4] = h;
     out[5] = a;
 }

@@ -5,8 +5,10 @@ mode) must agree within the north_star tolerance, 1e-9 relative in fp64, with
 exact test-error counts.  For the duality gap, which is a difference of two
 objectives of size ~0.1-1, the tolerance is taken relative to the primal:
 |gap - gap_ref| <= 1e-9 |P_ref|.  Problems are built by cocoa_amd.configs
-exactly as bench.py builds them (the same seeded generators); sizes are the
-full BASELINE sizes except where noted (C3 at 25,600 rows, C4 as one GPU's
+exactly as bench.py builds them (the same seeded generators).  Every line
+DESIGN.md publishes is parity-tested at the size it is benchmarked at: C2 /
+C5 at the full BASELINE size, C3 at n = 400,000 (and a 25,600-row cut for the
+quicker strict checks), C4 as the one-GPU K = 1,024 problem (and one GPU's
 strong-scaling share of the 8-GPU problem).
 Reference: CoCoA.scala:148-188 (local SDCA), MinibatchCD.scala:95-125,
 SGD.scala:104-135, OptUtils.scala:57-98.
@@ -204,6 +206,67 @@ def test_c4_fast_vs_oracle(c4):
     sh, od, ot = c4
     e = make_engine(sh, strict=False)
     e.init("cocoa+", sh.n_glob, 3, sh.H, sh.lam)
+    run = make_run(sh, od, "cocoa+")
+    for t in (1, 2, 3):
+        e.round(t)
+        run.round(t)
+    assert_close(e.eval(), run.eval(ot), True, 3)
+    assert_state_close(e, run, True)
+
+
+# ------------------------------------------- full-size published lines --
+@pytest.fixture(scope="module")
+def c3_full():
+    # the bench's C3 line: n = 400,000 dense rows of d = 2,000, K = 64, H = 6,250
+    sh = configs.share("c3")
+    return sh, odata(sh.train), odata(sh.test)
+
+
+@pytest.mark.timeout(900)
+def test_c3_full_strict_bitwise_vs_oracle(c3_full):
+    sh, od, ot = c3_full
+    assert sh.train.n == 400000 and sh.H == 6250
+    e = make_engine(sh, strict=True)
+    e.init("cocoa+", sh.n_glob, 2, sh.H, sh.lam)
+    run = make_run(sh, od, "cocoa+")
+    for t in (1, 2):
+        e.round(t)
+        run.round(t)
+    assert np.array_equal(e.w(), run.w())
+    assert np.array_equal(e.alpha(), run.alpha())
+    ev, rv = e.eval(), run.eval(ot)
+    assert ev["gap"].hex() == rv["gap"].hex()
+    assert ev["test_err_count"] == rv["test_err"]
+    del e
+
+
+@pytest.mark.timeout(900)
+def test_c3_full_fast_10_rounds_vs_oracle(c3_full):
+    sh, od, ot = c3_full
+    e = make_engine(sh, strict=False)
+    e.init("cocoa+", sh.n_glob, 10, sh.H, sh.lam)
+    assert e.plan()["solver"] == "dense"
+    run = make_run(sh, od, "cocoa+")
+    for t in range(1, 11):
+        e.round(t)
+        run.round(t)
+        if t % 5 == 0:
+            assert_close(e.eval(), run.eval(ot), True, t)
+    assert_state_close(e, run, True)
+    del e
+
+
+@pytest.mark.timeout(1200)
+def test_c4_one_gpu_k1024_fast_vs_oracle():
+    """The C4 one-GPU line: n = 2,396,130, d = 3,231,961, K = 1,024 on one
+    GPU (chain solver on compact deltaW slices), 3 rounds, exact error counts."""
+    sh = configs.share("c4", n_test=20000)
+    assert sh.k_glob == 1024 and sh.train.num_parts == 1024
+    od, ot = odata(sh.train), odata(sh.test)
+    e = make_engine(sh, strict=False)
+    e.init("cocoa+", sh.n_glob, 3, sh.H, sh.lam)
+    plan = e.plan()
+    assert plan["solver"] == "chain" and plan["dw_compact"] == 1, plan
     run = make_run(sh, od, "cocoa+")
     for t in (1, 2, 3):
         e.round(t)

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
         assert n in C.SIGNATURES, n
-    assert lib.cocoa_version() == 2
+    assert lib.cocoa_version() == 3
 
 
 def test_no_cpu_fallback_without_device():

@@ -1,0 +1,60 @@
+#!/bin/bash
+# GPU-box steps, run in order; the first failing step ends the call.
+#   tools/gpu_run.sh STEP [STEP ...]      (TAG=name labels the outputs)
+#   tests            pytest -m gpu (TESTS="-k expr" or a file list narrows it)
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench line (BENCH_ARGS adds flags)
+#   prof             rocprofv3 --kernel-trace --stats of a short bench
+#   pmc              FETCH_SIZE / WRITE_SIZE passes (+ calibration) of the same bench
+#   lines            the C5 / C3 / C4 config lines
+#   gramprof         Gram-solver wave profile (diag build, tools/prof_gram.py)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-now}
+O=gpurun_out
+SHORT="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-gap ${BENCH_ARGS}"
+
+line() {  # name, args...
+  local n=$1; shift
+  timeout -k 10 600 python3 bench.py "$@" > $O/line_$n.json 2> $O/line_$n.err || return $?
+  python3 -c "import json;d=json.loads(open('$O/line_$n.json').readlines()[-1]);print('$n', round(d['ms_per_step'],3), '%.4g'%d['value'], d['plan']['solver'], d.get('time_to_gap_s'), d.get('rounds_to_gap'), d['kernel_ms'])"
+}
+
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    tests)
+      timeout -k 10 1500 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
+        > $O/gpu_tests_$TAG.log 2>&1; rc=$?
+      grep -E "passed|failed|error" $O/gpu_tests_$TAG.log | tail -3; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 || exit $?
+      tail -1 $O/smoke_$TAG.log ;;
+    bench)
+      timeout -k 10 600 python3 bench.py ${BENCH_ARGS} > $O/bench_$TAG.json 2> $O/bench_$TAG.err || exit $?
+      tail -1 $O/bench_$TAG.json ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_$TAG -o run --output-format csv -- $SHORT \
+        > $O/rocprof_$TAG.log 2>&1 || exit $?
+      python3 tools/rocprof_stats.py $O/rocprof_$TAG ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc $c -d $O/pmc_${c}_$TAG -o run --output-format csv -- $SHORT \
+          > $O/pmc_${c}_$TAG.log 2>&1 || exit $?
+        timeout -s KILL 60 rocprofv3 --pmc $c -d $O/calib_${c}_$TAG -o run --output-format csv -- tools/ubench/calib \
+          > $O/calib_${c}_$TAG.log 2>&1 || exit $?
+      done ;;
+    lines)
+      line c5_cocoa --method cocoa --steps 10 --warmup 2 || exit $?
+      line c5_mbcd --method mbcd --steps 10 --warmup 2 || exit $?
+      line c5_mbsgd --method mbsgd --steps 10 --warmup 2 || exit $?
+      line c5_localsgd --method localsgd --steps 10 --warmup 2 || exit $?
+      line c3 --config c3 --steps 10 --warmup 2 || exit $?
+      line c4 --config c4 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+    gramprof)
+      COCOA_LIB=build/diag/libcocoa_hip.so timeout -k 10 200 python3 tools/prof_gram.py cocoa+ \
+        > $O/prof_gram_$TAG.json 2> $O/prof_gram_$TAG.err || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
