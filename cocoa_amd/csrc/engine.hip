@@ -165,6 +165,7 @@ struct cocoa_ctx {
     int32_t K_loc = 0, K_glob = 0, part_begin = 0, d = 0;
     Csr tr;
     DevBuf sqn, rowflags, part_ptr;
+    DevBuf row_z0;  // fast mode: entries of column class 0 per row (they lead the row), see set_train_impl
     std::vector<int64_t> h_part_ptr;
     bool any_dup = false;
     bool tr_dense = false;  // every row stores columns 0..d-1 in order (val = X[n][d])
@@ -236,7 +237,7 @@ struct cocoa_ctx {
         if (gstream) HIPCHK(hipStreamSynchronize(gstream));
         pre_t = -1;
     }
-    DevBuf plan_beg, plan_z, plan_y, plan_q, plan_xw;
+    DevBuf plan_beg, plan_z, plan_z0, plan_y, plan_q, plan_xw;
     // x.w of every train row for the current w, written by the fast eval pass
     // (eval v4) and reused by the next round's plan; false once w moves
     DevBuf row_xw;
@@ -709,6 +710,38 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
         pcol.resize((size_t)std::max<int64_t>(nnz, 1));
         for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];
     }
+    // Fast mode: every row stores the entries of column class 0 (even device
+    // column) before those of class 1, each class in stored order, so that the
+    // Gram solver's two memory waves (solver_gram.h) each stream one contiguous
+    // run per row.  Only the fast kernels see this order (their dots are
+    // reassociated anyway); strict mode keeps the stored order of every row.
+    std::vector<double> pval;
+    std::vector<int32_t> z0v;
+    const bool split_classes = !ctx->strict && !dense_in && !ctx->tr_dense && nnz > 0;  // dense rows: val is X[n][d]
+    if (split_classes) {
+        pval.resize((size_t)nnz);
+        z0v.resize((size_t)std::max<int64_t>(n_rows, 1));
+        std::vector<int32_t> ncol((size_t)std::max<int64_t>(nnz, 1));
+        const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        for (int tix = 0; tix < T; ++tix)
+            th.emplace_back([&, tix] {
+                for (int64_t r = n_rows * tix / T; r < n_rows * (tix + 1) / T; ++r) {
+                    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+                    int64_t c0 = 0;
+                    for (int64_t q = b; q < e; ++q) c0 += (pcol[(size_t)q] & 1) == 0;
+                    int64_t i0 = b, i1 = b + c0;
+                    for (int64_t q = b; q < e; ++q) {
+                        const int64_t dst = (pcol[(size_t)q] & 1) == 0 ? i0++ : i1++;
+                        ncol[(size_t)dst] = pcol[(size_t)q];
+                        pval[(size_t)dst] = val[q];
+                    }
+                    z0v[(size_t)r] = (int32_t)c0;
+                }
+            });
+        for (auto& t : th) t.join();
+        pcol.swap(ncol);
+    }
     hipStream_t s = ctx->stream;
     upload(ctx->d_perm, ctx->perm.data(), sizeof(int32_t) * (size_t)num_features, s);
     upload(ctx->d_inv, ctx->inv.data(), sizeof(int32_t) * (size_t)num_features, s);
@@ -721,7 +754,11 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
         upload_padded(ctx->tr.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
         upload_col16(ctx->tr.col16, pcol, nnz, num_features, s);
     }
-    upload_padded(ctx->tr.val, val, sizeof(double) * (size_t)nnz, s);
+    upload_padded(ctx->tr.val, split_classes ? pval.data() : val, sizeof(double) * (size_t)nnz, s);
+    if (split_classes)
+        upload(ctx->row_z0, z0v.data(), sizeof(int32_t) * (size_t)n_rows, s);
+    else
+        ctx->row_z0.free();
     upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
@@ -1039,6 +1076,10 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         const size_t steps = (size_t)std::max<int64_t>((int64_t)K * H, 1);
         ctx->plan_beg.alloc(steps * sizeof(int64_t));
         ctx->plan_z.alloc(steps * sizeof(int32_t));
+        if (ctx->row_z0.p)
+            ctx->plan_z0.alloc(steps * sizeof(int32_t));
+        else
+            ctx->plan_z0.free();
         ctx->plan_y.alloc(steps * sizeof(double));
         ctx->plan_q.alloc(steps * sizeof(double));
         ctx->plan_xw.alloc(steps * sizeof(double));
@@ -1050,6 +1091,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     } else {
         ctx->plan_beg.free();
         ctx->plan_z.free();
+        ctx->plan_z0.free();
         ctx->plan_y.free();
         ctx->plan_q.free();
         ctx->plan_xw.free();
@@ -1158,6 +1200,8 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             // the Gram solver splits x.w_local = x.w + x.deltaW
             pa.need_xw = !c->use_dense && (c->method != COCOA_METHOD_COCOA || c->use_gram);
             pa.xw_cache = (c->xw_cached && !c->strict) ? c->row_xw.as<double>() : nullptr;
+            pa.row_z0 = c->plan_z0.p ? c->row_z0.as<int32_t>() : nullptr;
+            pa.z0 = c->plan_z0.p ? c->plan_z0.as<int32_t>() : nullptr;
             pa.beg = c->plan_beg.as<int64_t>();
             pa.z = c->plan_z.as<int32_t>();
             pa.py = c->plan_y.as<double>();
@@ -1194,6 +1238,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.samples = smp;
             g.plan_beg = c->plan_beg.as<int64_t>();
             g.plan_z = c->plan_z.as<int32_t>();
+            g.plan_z0 = c->plan_z0.p ? c->plan_z0.as<int32_t>() : nullptr;
             g.plan_y = c->plan_y.as<double>();
             g.plan_q = c->plan_q.as<double>();
             g.plan_xw = c->plan_xw.as<double>();

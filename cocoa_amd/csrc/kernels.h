@@ -95,8 +95,10 @@ struct PlanArgs {
     int32_t H;
     int32_t need_xw;
     const double* xw_cache;   // per-row x.w of the current w from the last fast eval, or null
+    const int32_t* row_z0;    // per row: entries of column class 0 (fast mode), or null
     int64_t* beg;
     int32_t* z;
+    int32_t* z0;              // per step: row_z0 of its row (when row_z0)
     double* py;
     double* pq;
     double* xw;
@@ -120,6 +122,7 @@ struct GramSolverArgs {
     const int32_t* samples;
     const int64_t* plan_beg;
     const int32_t* plan_z;
+    const int32_t* plan_z0;   // per step: entries of column class 0 (they lead the row), or null: all
     const double* plan_y;
     const double* plan_q;
     const double* plan_xw;

@@ -131,13 +131,39 @@ __device__ __forceinline__ i32x4 load_cols(const int32_t* c32, const uint16_t* c
     return __builtin_nontemporal_load((const i32x4*)(c32 + k));
 }
 
-template <int TILE, int BLOCK, bool C16>
+// w gather of the fast eval: columns below HOT (device order: the most
+// frequent) from the block's LDS copy, the rest from global memory.  The two
+// are exclusive per lane (a branch, not a select), so the global gather
+// instruction only carries the cold lanes: the texture addresser processes a
+// gather lane by lane, and it -- not HBM -- bounds the pass (C2 PMC: TA busy
+// 80% of the kernel with every gather global).
+// (address-space-qualified accesses: with plain pointers the compiler merges
+// the two branches into one FLAT load on a selected pointer)
+typedef __attribute__((address_space(1))) const double gdouble;
+typedef __attribute__((address_space(3))) const double ldouble;
+template <int HOT>
+__device__ __forceinline__ double w_at(const double* w, const double* whot, int32_t c) {
+    double x;
+    if (HOT > 0 && c < HOT)
+        x = ((ldouble*)whot)[c];
+    else
+        x = ((gdouble*)w)[c];
+    return x;
+}
+
+template <int TILE, int BLOCK, bool C16, int DIAGW = 0, int HOT = 0>
 __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     constexpr int UNITS = TILE / (4 * BLOCK);  // 4-entry units per thread (base alignment adds one)
     __shared__ double prod[TILE + 4];
     __shared__ uint16_t roff[TILE + 2];
     __shared__ double red[BLOCK / 64];
+    __shared__ double whot[HOT > 0 ? HOT : 1];
     const int tid = threadIdx.x;
+    if (HOT > 0) {
+        const int32_t h = (int32_t)min<int64_t>(HOT, a.d);
+        for (int32_t j = tid; j < h; j += BLOCK) whot[j] = a.w[j];
+        __syncthreads();
+    }
     const int sub = tid & 15, grp = tid >> 4;
     double hinge = 0.0, err = 0.0;
     const int64_t ntiles = a.n_tiles + a.n_t_tiles;
@@ -183,6 +209,8 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             v1[u] = v0[u];
             if (k < span) {
                 c[u] = load_cols<C16>(cl, cl16, base + k);
+                if (DIAGW == 1) c[u] &= 4095;  // timing diagnostic only: every gather in a 32 KB window
+                if (DIAGW == 2) c[u] &= 0;     // timing diagnostic only: one address
                 v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
                 v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
             }
@@ -192,8 +220,8 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
             if (k < span) {
                 // entries past e1 inside the last unit are never summed (roff bounds rows)
-                *(f64x2*)(prod + k) = f64x2{v0[u].x * a.w[c[u].x], v0[u].y * a.w[c[u].y]};
-                *(f64x2*)(prod + k + 2) = f64x2{v1[u].x * a.w[c[u].z], v1[u].y * a.w[c[u].w]};
+                *(f64x2*)(prod + k) = f64x2{v0[u].x * w_at<HOT>(a.w, whot, c[u].x), v0[u].y * w_at<HOT>(a.w, whot, c[u].y)};
+                *(f64x2*)(prod + k + 2) = f64x2{v1[u].x * w_at<HOT>(a.w, whot, c[u].z), v1[u].y * w_at<HOT>(a.w, whot, c[u].w)};
             }
         }
         __syncthreads();
@@ -231,6 +259,70 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     }
 }
 
+// Row-parallel variant: one 16-lane group per row, straight from global memory
+// (no LDS staging, no barriers), U loads per lane in flight per row chunk,
+// rows walked grid-stride so every wave always has rows of its own in flight.
+// Every load stays in bounds (a lane past the row reloads the row's last
+// entry and drops it), so the compiler issues a chunk's loads back to back.
+template <int U, bool C16>
+__global__ __launch_bounds__(256) void eval_rows_kernel(EvalArgs a) {
+    constexpr int G = 16;
+    __shared__ double red[4];
+    const int tid = threadIdx.x, lane = tid & 63, sub = lane & (G - 1);
+    const int64_t rows = a.n + a.n_test;
+    const int64_t ng = (int64_t)gridDim.x * (256 / G);
+    double hinge = 0.0, err = 0.0;
+    for (int64_t r = ((int64_t)blockIdx.x * 256 + tid) / G; r < rows; r += ng) {
+        const bool test = r >= a.n;
+        const int64_t rr = test ? r - a.n : r;
+        const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
+        const int32_t* cl = test ? a.t_col : a.col;
+        const uint16_t* cl16 = test ? a.t_col16 : a.col16;
+        const double* vl = test ? a.t_val : a.val;
+        const int64_t b = rp[rr], e = rp[rr + 1];
+        double acc = 0.0;
+        for (int64_t q0 = b; q0 < e; q0 += G * U) {
+            int32_t c[U];
+            double v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t q = min(q0 + u * G + sub, e - 1);
+                c[u] = C16 ? (int32_t)__builtin_nontemporal_load(cl16 + q) : __builtin_nontemporal_load(cl + q);
+                v[u] = __builtin_nontemporal_load(vl + q);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double x = a.w[c[u]];
+                acc = fma(q0 + u * G + sub < e ? v[u] : 0.0, x, acc);
+            }
+        }
+        const double dot = row16_sum(acc);
+        if (sub == 0) {
+            if (!test) {
+                hinge += jmax(1 - a.y[rr] * dot, 0.0);          // OptUtils.scala:57-61
+                if (a.row_xw) a.row_xw[rr] = dot;
+            } else {
+                err += (dot * a.t_y[rr] > 0) ? 0.0 : 1.0;        // OptUtils.scala:95-98
+            }
+        }
+    }
+    const int64_t gt = (int64_t)blockIdx.x * 256 + tid, gs = (int64_t)gridDim.x * 256;
+    double al = 0.0, w2 = 0.0;
+    for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
+    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
+    const double s0 = block_sum_n<256>(hinge, red);
+    const double s1 = block_sum_n<256>(al, red);
+    const double s2 = block_sum_n<256>(w2, red);
+    const double s3 = block_sum_n<256>(err, red);
+    if (tid == 0) {
+        double* p = a.partials + (size_t)blockIdx.x * 4;
+        p[0] = s0;
+        p[1] = s1;
+        p[2] = s2;
+        p[3] = s3;
+    }
+}
+
 __global__ __launch_bounds__(256) void eval_final_kernel(const double* partials, int blocks, double* out) {
     __shared__ double red[4][4];
     const int tid = threadIdx.x;
@@ -253,16 +345,78 @@ int eval_fast_blocks(int64_t n_tiles, int64_t n_t_tiles) {
     return (int)(b < 1 ? 1 : b);
 }
 
+static int eval_variant();
 int eval_tile_entries() {
 #ifdef COCOA_DIAG
     // diagnostic builds only (make diag): A/B of the tile size
     if (const char* e = getenv("COCOA_EVAL_TILE")) return atoi(e) == 2048 ? 2048 : kEvalTile;
 #endif
-    return kEvalTile;
+    return (eval_variant() >= 6 && eval_variant() <= 9) ? 2048 : kEvalTile;
+}
+
+// eval variant (A/B while measuring): 0 = row tiles through LDS, 1 = rows
+// from global with 8 loads per lane in flight, 2 = 4 loads
+static int eval_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("COCOA_EVAL_VARIANT");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
 }
 
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
     const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
+    if (eval_variant() == 8 || eval_variant() == 9) {  // 2,048-entry tiles, more blocks per CU
+        const int64_t nt = a.n_tiles + a.n_t_tiles;
+        if (eval_variant() == 8) {  // 512 threads, 4 blocks per CU
+            const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(nt, 1024));
+            if (c16) eval_stream_kernel<2048, 512, true><<<nb, 512, 0, s>>>(a);
+            else eval_stream_kernel<2048, 512, false><<<nb, 512, 0, s>>>(a);
+            eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
+        } else {  // 256 threads, 8 blocks per CU
+            const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(nt, 2048));
+            if (c16) eval_stream_kernel<2048, 256, true><<<nb, 256, 0, s>>>(a);
+            else eval_stream_kernel<2048, 256, false><<<nb, 256, 0, s>>>(a);
+            eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
+        }
+        return;
+    }
+    if (eval_variant() >= 5) {  // hot w columns in LDS
+        const int nb = eval_fast_blocks(a.n_tiles, a.n_t_tiles);
+        if (eval_variant() == 5) {  // 4,096-entry tiles, 32 KB of w: 2 blocks per CU
+            const int n2 = (int)std::min<int64_t>(a.n_tiles + a.n_t_tiles, 512);
+            eval_stream_kernel<kEvalTile, 512, true, 0, 4096><<<n2, 512, 0, s>>>(a);
+            eval_final_kernel<<<1, 256, 0, s>>>(a.partials, n2, a.out);
+        } else if (eval_variant() == 6) {  // 2,048-entry tiles, 32 KB of w: 3 blocks per CU
+            eval_stream_kernel<2048, 512, true, 0, 4096><<<nb, 512, 0, s>>>(a);
+            eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
+        } else {  // 2,048-entry tiles, 64 KB of w (8,192 columns): 2 blocks per CU
+            const int n2 = (int)std::min<int64_t>(a.n_tiles + a.n_t_tiles, 512);
+            eval_stream_kernel<2048, 512, true, 0, 8192><<<n2, 512, 0, s>>>(a);
+            eval_final_kernel<<<1, 256, 0, s>>>(a.partials, n2, a.out);
+        }
+        return;
+    }
+    if (eval_variant() >= 3) {  // timing diagnostics (results invalid)
+        const int nb = eval_fast_blocks(a.n_tiles, a.n_t_tiles);
+        if (eval_variant() == 3) eval_stream_kernel<kEvalTile, 512, true, 1><<<nb, 512, 0, s>>>(a);
+        else eval_stream_kernel<kEvalTile, 512, true, 2><<<nb, 512, 0, s>>>(a);
+        eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
+        return;
+    }
+    if (eval_variant() != 0) {
+        const int nb = 2048;  // 8 blocks of 256 threads per CU, persistent
+        if (eval_variant() == 1) {
+            if (c16) eval_rows_kernel<8, true><<<nb, 256, 0, s>>>(a);
+            else eval_rows_kernel<8, false><<<nb, 256, 0, s>>>(a);
+        } else {
+            if (c16) eval_rows_kernel<4, true><<<nb, 256, 0, s>>>(a);
+            else eval_rows_kernel<4, false><<<nb, 256, 0, s>>>(a);
+        }
+        eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
+        return;
+    }
     if (eval_tile_entries() == 2048) {
         if (c16) eval_stream_kernel<2048, 512, true><<<blocks, 512, 0, s>>>(a);
         else eval_stream_kernel<2048, 512, false><<<blocks, 512, 0, s>>>(a);

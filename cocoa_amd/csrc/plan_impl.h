@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         __builtin_nontemporal_store(a.y[gr], a.py + g);
         __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
         __builtin_nontemporal_store(xw, a.xw + g);
+        if (a.row_z0) __builtin_nontemporal_store(a.row_z0[gr], a.z0 + g);
     }
 }
 

@@ -22,24 +22,29 @@
 // rule, and adds c_j * G(., j) to every pending lane -- one FMA, no memory
 // access and no reduction on the dependent path.
 //
-// Roles (one 256-thread workgroup per partition, one wave each):
-//   wave 0  chain  -- the H sequential steps (update rule, alpha in LDS);
-//   wave 1  memory -- per batch b: deltaW += c_j x_j for the steps of batch b
-//                     (fp64 atomics into the partition's private slice), then
-//                     the gathers of x_s . deltaW for batch b+4, software-
-//                     pipelined one batch deep (issued now, summed next time);
-//   wave 2  loader -- per-step records (constants of the update rule, the
-//                     next occurrence of the same row in the window).
+// Roles (one 384-thread workgroup per partition, one wave each):
+//   chain      -- the H sequential steps (update rule, alpha in LDS);
+//   memory x2  -- one per column class (device column parity): per batch b,
+//                 deltaW += c_j x_j for the steps of batch b on the class's
+//                 columns (fp64 atomics into the partition's private slice),
+//                 then the gathers of x_s . deltaW for batch b+4 on them,
+//                 software-pipelined one batch deep (issued now, summed next
+//                 time) into the class's partial base;
+//   loader     -- per-step records (constants of the update rule, the next
+//                 occurrence of the same row in the window) and row layouts;
+//   fetch x2   -- one per class: LDS DMA of the batch's class entries into the
+//                 class's sub-ring.
 // The waves hand off through counters in LDS (release / acquire, s_sleep
 // while waiting), not workgroup barriers, so the chain never waits on a
 // helper that is merely busy with a later batch.
 //
 // Ordering of the deltaW slice: base(b) must contain exactly the updates of
-// batches <= b-4.  The memory wave issues, in this order, the atomics of
-// batch b-4 and then the gathers of base(b), and the atomics of batch b-3
-// only after those gathers: one wave, one address stream, so the gathers see
-// batch b-4 and nothing later.  Batches b-3 .. b reach the steps of batch b
-// through the Gram corrections (window of 64 steps = 4 batches of 16).
+// batches <= b-4.  A column belongs to one class, so one memory wave issues,
+// in this order, the atomics of batch b-4 to it and then the gathers of
+// base(b), and the atomics of batch b-3 only after those gathers: one wave,
+// one address stream, so the gathers see batch b-4 and nothing later.
+// Batches b-3 .. b reach the steps of batch b through the Gram corrections
+// (window of 64 steps = 4 batches of 16).
 //
 // Numerics: fast mode (fused multiply-adds, reassociated dots, atomics); the
 // results agree with the strict path / oracle within the north_star
@@ -376,14 +381,30 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
 // u >= aa; that is the PROJ variant of the kernel.  An empty row (qii = 0) has
 // grad = -lambda n < 0 and gets alpha = 1 unless skipped: B = 0 and E = -1e300,
 // so u is huge for any aa.  MbCD (MinibatchCD.scala:104): A = 0, so B = 0.
+//
+// Column classes.  deltaW's columns are split into kGNC classes (device
+// column parity: the device order is by frequency, so the classes carry
+// about the same entries); in fast mode every row stores its class-0 entries
+// first (cocoa_set_train), so a row's entries of one class are one contiguous
+// run.  Each class has its own fetch wave, LDS sub-ring and memory wave: the
+// memory wave of class c scatters and gathers only columns of class c, so the
+// per-column order "scatter of batch b, then gathers of batch b+4" still holds
+// inside one wave's address stream, and the two memory waves -- the issue-
+// bound part of the round -- run on different SIMDs.  The chain adds the two
+// partial bases.
 constexpr int kGWin = kGSlots + kGB;     // loader's look-back for alpha forwarding: 5 batches
-constexpr int kGE = 8192;                // staged entries (LDS ring positions)
+constexpr int kGNC = 2;                  // column classes = memory waves = fetch waves
+constexpr int kGE = 8192;                // staged entries (LDS ring positions), all classes
+constexpr int kGSub = kGE / 64 / kGNC;   // 64-entry units of one class's sub-ring
 constexpr int kGUnitB = 64 * 13;         // bytes of one 64-entry ring unit
 constexpr int kGOCol = 0, kGOLo = 256, kGOHi = 512, kGORow = 768;  // its fields
-constexpr int kGMaxU = 32;               // 64-entry units of a staged batch; larger batches go direct
-constexpr int kGFetch = 2;               // fetch waves
-constexpr int kGThreads = 64 * (3 + kGFetch);
+constexpr int kGMaxU = kGSub / 4;        // units of one class of a staged batch (4 live batches per
+                                         // sub-ring); larger batches go direct
+constexpr int kGThreads = 64 * (2 + 2 * kGNC);
 constexpr int kGGt = 4;                  // Gram-row ring (batches)
+constexpr int kGPart = 32;               // product slots per row (lanes l and l + 32 share one)
+// wave roles (waves w and w + 4 share a SIMD: the memory waves get one each)
+constexpr int kWChain = 0, kWFetch0 = 1, kWMem0 = 2, kWMem1 = 3, kWLoader = 4, kWFetch1 = 5;
 
 struct GRec {                          // one step (64 B)
     double B, Y, AE, YA;               // AE, YA: set by the chain (its alpha prefetch or a forward)
@@ -396,30 +417,33 @@ struct GRec {                          // one step (64 B)
 };
 static_assert(sizeof(GRec) == 64, "GRec layout");
 
-struct GLay {                          // one batch's rows, for the fetch and memory waves
-    int64_t sb[kGB];                   // row starts in the CSR
+struct GLay {                          // one batch's rows of one class, for the fetch and memory waves
+    int64_t sb[kGB];                   // starts of the rows' class runs in the CSR
     int32_t sx[kGB + 1];               // packed offsets: row i at [sx[i], sx[i+1])
-    int32_t pos;                       // ring position of the staged entries (multiple of 64); -1: direct
+    int32_t pos;                       // sub-ring position of the staged entries (multiple of 64); -1: direct
     int32_t nu;                        // 64-entry units
     int32_t T;                         // entries
 };
 
-// counters (LDS, release / acquire)
-constexpr int kCChain = 0, kCScat = 1, kCBase = 2, kCLoad = 3, kCAbort = 4, kCFreed = 5, kCFetch = 6;
+// counters (LDS, release / acquire); kCScat .. kCFetch: one per class
+constexpr int kCChain = 0, kCLoad = 1, kCAbort = 2, kCScat = 3, kCBase = kCScat + kGNC, kCFreed = kCBase + kGNC,
+              kCFetch = kCFreed + kGNC;
+static_assert(kCFetch + kGNC <= 16, "counters");
 
 struct GramSolverLds {
     int cnt[16];
     GRec rec[kGRing * kGB];            // ring: (b % kGRing) * kGB + i
-    double coef[kGRing * 2 * kGB];     // c_j, same ring (chain -> memory wave); [kGB, 2 kGB) of a slot stay 0
-    GLay lay[kGRing];                  // same ring (loader -> fetch / memory waves)
-    double base[kGSlots];              // base_s per slot (memory wave -> chain)
-    double part[kGB + 1][64];          // memory wave: per-lane row partial sums of a batch's products (+ a sink row)
+    double coef[kGRing * 2 * kGB];     // c_j, same ring (chain -> memory waves); [kGB, 2 kGB) of a slot stay 0
+    GLay lay[kGRing][kGNC];            // same ring (loader -> fetch / memory waves)
+    double base[kGNC][kGSlots];        // partial base_s per class and slot (memory waves -> chain)
+    double part[kGNC][kGB + 1][kGPart];  // memory wave: row partial sums of a batch's products (+ a sink row)
     double gring[kGGt][kGB][kGSlots];  // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
     int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
-    // staged entries (fetch waves -> memory wave), 64 per ring unit: columns, value
+    // staged entries (fetch waves -> memory waves), 64 per ring unit: columns, value
     // low words, value high words (the LDS DMA moves 4 bytes a lane), row bytes
     // (0xFF: past the batch's entries).  One address per lane and unit reaches all
-    // four (immediate offsets; the two value words in one ds_read2).
+    // four (immediate offsets; the two value words in one ds_read2).  Class c owns
+    // units [c kGSub, (c + 1) kGSub).
     alignas(16) uint8_t ring[kGE / 64][kGUnitB];
 };
 
@@ -462,8 +486,10 @@ __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
 __device__ __forceinline__ uint32_t gram_pad(int32_t u, int32_t nu) {
     return (uint32_t)((nu - 1 - u) >> 31) & 0xFFu;
 }
-// ring unit of entry position pos (a multiple of 64) + 64 u
-__device__ __forceinline__ int32_t ring_unit(int32_t pos, int32_t u) { return ((pos >> 6) + u) & (kGE / 64 - 1); }
+// ring unit of class c's sub-ring position pos (a multiple of 64) + 64 u
+__device__ __forceinline__ int32_t ring_unit(int c, int32_t pos, int32_t u) {
+    return c * kGSub + (((pos >> 6) + u) & (kGSub - 1));
+}
 // lane's entry of a ring unit: (column, value, row byte)
 __device__ __forceinline__ void ring_get(const GramSolverLds& S, int32_t us, int lane, int32_t& col, double& val,
                                          uint32_t& row) {
@@ -473,15 +499,6 @@ __device__ __forceinline__ void ring_get(const GramSolverLds& S, int32_t us, int
     row = b[kGORow + lane];
 }
 
-// Roles (kGThreads threads, one workgroup per partition):
-//   wave 0       chain  -- the H dependent steps;
-//   wave 1       memory -- per batch b: deltaW += c_j x_j (batch b), then the
-//                          gathers x_s . deltaW of batch b+4, their products
-//                          summed one batch later;
-//   wave 2       loader -- records (update-rule constants, alpha forwarding
-//                          marks) and row layouts, up to kGRing batches ahead;
-//   waves 3..    fetch  -- copy each batch's (column, value) entries into the
-//                          LDS ring (LDS DMA), ahead of the gathers.
 // CoCoA.scala:166-178 on u = aa - grad / qii: the clamp, and with PROJ the
 // projected-gradient skip for an alpha outside [0, 1]
 template <bool PROJ>
@@ -492,6 +509,15 @@ __device__ __forceinline__ double gram_rule(double u, double aa) {
     return skip ? aa : nt;
 }
 
+// Roles (kGThreads threads, one workgroup per partition):
+//   chain        -- the H dependent steps;
+//   memory c     -- per batch b: deltaW += c_j x_j on class-c columns (batch b),
+//                   then the gathers x_s . deltaW of batch b+4 on class-c columns,
+//                   their products summed one batch later into base[c];
+//   loader       -- records (update-rule constants, alpha forwarding marks) and
+//                   the per-class row layouts, up to kGRing batches ahead;
+//   fetch c      -- copy each batch's class-c (column, value) entries into the
+//                   class's LDS sub-ring (LDS DMA), ahead of the gathers.
 template <int MODE, bool HOTLDS, bool PROJ>
 __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -513,30 +539,32 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 
     for (int32_t i = tid; i < nl; i += kGThreads) alv[i] = a.alpha[p0 + i];
     if (tid == 0) alv[nl] = 0.0;
-    for (int i = tid; i < kGSlots; i += kGThreads) S.base[i] = 0.0;  // batches 0 .. kGNB-1: deltaW is still zero
+    for (int i = tid; i < kGNC * kGSlots; i += kGThreads) (&S.base[0][0])[i] = 0.0;  // batches 0 .. kGNB-1
     for (int32_t i = tid; i < hot; i += kGThreads) hotl[i] = 0.0;
     for (int i = tid; i < kGRing * 2 * kGB; i += kGThreads) S.coef[i] = 0.0;  // zero slots: rows past a batch
     if (tid < 16) S.cnt[tid] = 0;
     __syncthreads();
-    if (tid == 0) S.cnt[kCBase] = kGNB;
+    if (tid < kGNC) S.cnt[kCBase + tid] = kGNB;
     __syncthreads();
     uint64_t wait_cycles = 0;
     uint64_t* pw = a.prof ? &wait_cycles : nullptr;
     const uint64_t t_start = a.prof ? __builtin_readcyclecounter() : 0;
 
-    if (wv == 2) {
+    if (wv == kWLoader) {
         // ------------------------------------------------------- loader --
-        int32_t cursor = 0;  // ring position of the next staged batch
+        int32_t cursor[kGNC];  // sub-ring position of the next staged batch, per class
+#pragma unroll
+        for (int c = 0; c < kGNC; ++c) cursor[c] = 0;
         for (int i = lane; i < 2 * kGSlots; i += 64) S.smpwin[i] = -2;
         // the step's inputs one batch ahead (registers)
         const int i = lane & (kGB - 1);
-        int32_t xr = nl, xz = 0;
+        int32_t xr = nl, xz = 0, xz0 = 0;
         double xy = 0.0, xq = 0.0, xxw = 0.0;
         int64_t xbeg = 0;
         auto load = [&](int32_t b) {
             const int32_t j = b * kGB + i;
             xr = nl;
-            xz = 0;
+            xz = xz0 = 0;
             xy = xq = xxw = 0.0;
             xbeg = 0;
             if (lane < kGB && j < H) {
@@ -546,31 +574,42 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 xxw = a.plan_xw[g0 + j];
                 xbeg = a.plan_beg[g0 + j];
                 xz = a.plan_z[g0 + j];
+                xz0 = a.plan_z0 ? a.plan_z0[g0 + j] : xz;
             }
         };
         load(0);
-        // batch b's records and layout; the Gram rows of batch b-4 (LDS DMA, their
+        // batch b's records and layouts; the Gram rows of batch b-4 (LDS DMA, their
         // completion published one iteration later: kCLoad = b+1 means records
         // <= b and Gram rows <= b-5 are in LDS)
         const int32_t NL = MODE != MODE_MBCD ? NB + kGGt + 1 : NB;
         for (int32_t b = 0; b < NL; ++b) {
             // ring slots (records b % kGRing, Gram rows (b-4) % kGGt) last held batch
-            // b - kGRing: chain and memory wave done with it
+            // b - kGRing: chain and both memory waves done with it
             if (!wait_ge(&S.cnt[kCChain], b - kGRing + 1, abortf, a.status, pw)) break;
-            if (!wait_ge(&S.cnt[kCScat], min(b, NB) - kGRing + 1, abortf, a.status, pw)) break;
+            bool ok = true;
+#pragma unroll
+            for (int c = 0; c < kGNC; ++c)
+                ok = ok && wait_ge(&S.cnt[kCScat + c], min(b, NB) - kGRing + 1, abortf, a.status, pw);
+            if (!ok) break;
             vm_drain();  // last iteration's loads and DMA
             if (b < NB) {
                 const int32_t j = b * kGB + i;
                 const bool valid = lane < kGB && j < H;
-                const int32_t r = xr, z = xz;
+                const int32_t r = xr, z = xz, z0 = xz0;
                 const double y = xy, q = xq, xw = xxw;
                 const int64_t beg = xbeg;
                 if (b + 1 < NB) load(b + 1);
                 const int32_t w0 = b * kGB - kGSlots;  // look-back window: steps [w0, w0 + kGWin)
                 if (lane < kGB) S.smpwin[j & (2 * kGSlots - 1)] = valid ? r : -2;
-                const int32_t inc = wave_incl_scan(lane < kGB ? z : 0);
-                const int32_t T = __shfl(inc, kGB - 1, 64);
-                const int32_t nu = (T + 63) >> 6;
+                // the rows' runs of each class: class 0 = entries [beg, beg + z0), class 1 = the rest
+                int32_t inc[kGNC], T[kGNC], nu[kGNC];
+#pragma unroll
+                for (int c = 0; c < kGNC; ++c) {
+                    const int32_t zc = c == 0 ? z0 : z - z0;
+                    inc[c] = wave_incl_scan(lane < kGB ? zc : 0);
+                    T[c] = __shfl(inc[c], kGB - 1, 64);
+                    nu[c] = (T[c] + 63) >> 6;
+                }
                 wave_lds_sync();
                 // previous occurrence of each step's row in the window before it: lanes =
                 // window positions (0..63: batches b-4 .. b-1; 64 + lane: this batch)
@@ -587,7 +626,6 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         if (lane == t) pd = p;
                     }
                 }
-                GLay& L = S.lay[b % kGRing];
                 if (lane < kGB) {
                     GRec& R = S.rec[(b % kGRing) * kGB + lane];
                     double B = 0.0, E = 0.0, Y = 0.0;
@@ -598,16 +636,22 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     R.r = r;
                     R.fw = -1;
                     R.fwd = 0;
-                    L.sx[lane + 1] = inc;
-                    L.sb[lane] = beg;
                 }
-                if (lane == 0) {
-                    L.sx[0] = 0;
-                    L.T = T;
-                    L.nu = nu;
-                    L.pos = nu <= kGMaxU ? cursor : -1;
+#pragma unroll
+                for (int c = 0; c < kGNC; ++c) {
+                    GLay& L = S.lay[b % kGRing][c];
+                    if (lane < kGB) {
+                        L.sx[lane + 1] = inc[c];
+                        L.sb[lane] = c == 0 ? beg : beg + z0;
+                    }
+                    if (lane == 0) {
+                        L.sx[0] = 0;
+                        L.T = T[c];
+                        L.nu = nu[c];
+                        L.pos = nu[c] <= kGMaxU ? cursor[c] : -1;
+                    }
+                    if (nu[c] <= kGMaxU) cursor[c] += nu[c] * 64;
                 }
-                if (nu <= kGMaxU) cursor += nu * 64;
                 wave_lds_sync();
                 // mark the earlier occurrence: step w0 + pd forwards its new alpha here
                 if (lane < kGB && pd >= 0) {
@@ -625,19 +669,19 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCLoad], b + 1);
         }
-    } else if (wv >= 3) {
+    } else if (wv == kWFetch0 || wv == kWFetch1) {
         // -------------------------------------------------------- fetch --
-        const int f = wv - 3;
-        for (int32_t x = f; x < NB; x += kGFetch) {
+        const int c = wv == kWFetch0 ? 0 : 1;
+        for (int32_t x = 0; x < NB; ++x) {
             if (!wait_ge(&S.cnt[kCLoad], x + 1, abortf, a.status, pw)) break;
-            const GLay& L = S.lay[x % kGRing];
+            const GLay& L = S.lay[x % kGRing][c];
             const int32_t pos = L.pos, nu = L.nu, T = L.T;
             if (pos >= 0 && nu > 0) {
-                // ring space: positions up to pos + 64 nu - kGE released by the memory wave
-                if (!wait_ge(&S.cnt[kCFreed], pos + nu * 64 - kGE, abortf, a.status, pw)) break;
+                // sub-ring space: positions up to pos + 64 nu - 64 kGSub released by the memory wave
+                if (!wait_ge(&S.cnt[kCFreed + c], pos + nu * 64 - kGSub * 64, abortf, a.status, pw)) break;
                 for (int32_t u = 0; u < nu; ++u) {
                     const int32_t q = u * 64 + lane;
-                    uint8_t* ub = S.ring[ring_unit(pos, u)];
+                    uint8_t* ub = S.ring[ring_unit(c, pos, u)];
                     const int o = gram_owner(L.sx, q);
                     if (q < T) {
                         const int64_t e = L.sb[o] + (q - L.sx[o]);
@@ -650,23 +694,23 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 vm_drain();  // the DMA writes are in LDS
             }
             wave_lds_sync();
-            if (lane == 0) lds_release(&S.cnt[kCFetch + f], x + 1);
+            if (lane == 0) lds_release(&S.cnt[kCFetch + c], x + 1);
         }
-    } else if (wv == 1) {
+    } else if (wv == kWMem0 || wv == kWMem1) {
         // ------------------------------------------------------- memory --
+        const int c = wv == kWMem0 ? 0 : 1;  // this wave's column class
         const bool bases = MODE != MODE_MBCD;
         double hv[kGMaxU], dw[kGMaxU];  // in-flight gathers: staged value (x hot deltaW), loaded deltaW (or 1)
         uint32_t hrow[(kGMaxU + 5) / 6];  //   and their rows (5 bits per unit, 31 = no entry)
         int32_t xin = -1;               // batch whose gathers are in flight
         int32_t xnu = 0;                //   and its 64-entry units
-        auto dw_add = [&](int32_t c, double v) {
-            if (HOTLDS && c < hot) __hip_atomic_fetch_add(hotl + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else unsafeAtomicAdd(dwk + c, v);
+        double(*part)[kGPart] = S.part[c];
+        auto dw_add = [&](int32_t col, double v) {
+            if (HOTLDS && col < hot) __hip_atomic_fetch_add(hotl + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else unsafeAtomicAdd(dwk + col, v);
         };
-        auto dw_get = [&](int32_t c) { return (HOTLDS && c < hot) ? hotl[c] : dw_load(dwk + c); };
-        auto fetched = [&](int32_t x) {
-            return wait_ge(&S.cnt[kCFetch + x % kGFetch], x + 1, abortf, a.status, pw);
-        };
+        auto dw_get = [&](int32_t col) { return (HOTLDS && col < hot) ? hotl[col] : dw_load(dwk + col); };
+        auto fetched = [&](int32_t x) { return wait_ge(&S.cnt[kCFetch + c], x + 1, abortf, a.status, pw); };
         uint64_t ph[4] = {0, 0, 0, 0};
         uint64_t tph = 0;
         auto stamp = [&](int i) {
@@ -683,39 +727,41 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             // anyway): the compiler then knows no register is still being written and
             // issues step 3's loads back to back instead of waiting before each one
             vm_drain();
-            // 1. products of the gathers in flight -> base of batch xin.  Each lane
-            //    runs over its positions (rows ascend with the unit) and parks one
-            //    partial sum per (row, lane); 4 lanes per row add them up.
+            // 1. products of the gathers in flight -> this class's part of the base of
+            //    batch xin.  Each unit's product goes to (its row, lane mod 32) with a
+            //    fire-and-forget LDS add (lanes l and l + 32 share a slot: different
+            //    LDS lane groups, no conflict); 4 lanes per row add the slots up.
             if (xin >= 0) {
+                if (lane < kGPart) {
 #pragma unroll
-                for (int i = 0; i < kGB; ++i) S.part[i][lane] = 0.0;
-                // every unit adds its product into (its row, this lane): a fire-and-forget
-                // LDS add per unit, no branch (entries past the batch go to the sink row);
-                // the units past the batch are skipped as a whole (uniform branch)
+                    for (int i = 0; i < kGB; ++i) part[i][lane] = 0.0;
+                }
+                wave_lds_sync();
 #pragma unroll
                 for (int u = 0; u < kGMaxU; ++u) {
                     if (u < xnu) {
                         const int row = min((int)((hrow[u / 6] >> (5 * (u % 6))) & 31u), kGB);  // 31: no entry
-                        __hip_atomic_fetch_add(&S.part[row][lane], hv[u] * dw[u], __ATOMIC_RELAXED,
+                        __hip_atomic_fetch_add(&part[row][lane & (kGPart - 1)], hv[u] * dw[u], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
                 wave_lds_sync();
-                const int rr = lane >> 2, qq = (lane & 3) * 16;
+                const int rr = lane >> 2, qq = (lane & 3) * (kGPart / 4);
                 double s4 = 0.0;
 #pragma unroll
-                for (int t = 0; t < 16; ++t) s4 += S.part[rr][qq + t];
+                for (int t = 0; t < kGPart / 4; ++t) s4 += part[rr][qq + t];
                 s4 += dpp_row_d<0xB1>(s4);  // quad_perm [1,0,3,2]
                 s4 += dpp_row_d<0x4E>(s4);  // quad_perm [2,3,0,1]
-                if ((lane & 3) == 0) S.base[(xin % kGNB) * kGB + rr] = s4;
+                if ((lane & 3) == 0) S.base[c][(xin % kGNB) * kGB + rr] = s4;
                 wave_lds_sync();
-                if (lane == 0) lds_release(&S.cnt[kCBase], xin + 1);
+                if (lane == 0) lds_release(&S.cnt[kCBase + c], xin + 1);
                 xin = -1;
             }
             stamp(0);
-            // 2. deltaW += c_j x_j for the steps of batch b (CoCoA.scala:181-185)
+            // 2. deltaW += c_j x_j on this class's columns for the steps of batch b
+            //    (CoCoA.scala:181-185)
             {
-                const GLay& L = S.lay[b % kGRing];
+                const GLay& L = S.lay[b % kGRing][c];
                 const double* cf = S.coef + (b % kGRing) * (2 * kGB);
                 const int32_t pos = L.pos, nu = L.nu;
                 if (pos >= 0) {
@@ -731,7 +777,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 #pragma unroll
                         for (int t = 0; t < 8; ++t) {
                             uint32_t r8;
-                            ring_get(S, ring_unit(pos, u0 + t), lane, cl[t], vl[t], r8);
+                            ring_get(S, ring_unit(c, pos, u0 + t), lane, cl[t], vl[t], r8);
                             rw[t] = r8 | gram_pad(u0 + t, nu);
                         }
 #pragma unroll
@@ -744,33 +790,32 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 } else {
                     // a batch too long to stage: straight from the CSR, row by row
                     for (int i = 0; i < kGB; ++i) {
-                        const double c = cf[i];
-                        if (c == 0.0) continue;
+                        const double cv = cf[i];
+                        if (cv == 0.0) continue;
                         const int32_t z = L.sx[i + 1] - L.sx[i];
                         const int64_t rb = L.sb[i];
-                        for (int32_t e = lane; e < z; e += 64) dw_add(a.col[rb + e], a.val[rb + e] * c);
+                        for (int32_t e = lane; e < z; e += 64) dw_add(a.col[rb + e], a.val[rb + e] * cv);
                     }
                 }
                 wave_lds_sync();
                 if (lane == 0) {
-                    lds_release(&S.cnt[kCScat], b + 1);  // coefficient / record / layout slot consumed
-                    if (pos >= 0) lds_release(&S.cnt[kCFreed], pos + nu * 64);
+                    lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
+                    if (pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
                 }
             }
             stamp(1);
-            // 3. gathers of batch x = b + kGNB: they see batch b's updates (issued
-            //    above, same wave, same addresses) and nothing later (the next
-            //    atomics go out after step 1 has consumed these loads)
+            // 3. gathers of batch x = b + kGNB on this class's columns: they see batch
+            //    b's updates (issued above, same wave, same addresses) and nothing later
+            //    (the next atomics go out after step 1 has consumed these loads)
             const int32_t x = b + kGNB;
             if (bases && x < NB) {
-                const GLay& L = S.lay[x % kGRing];
+                const GLay& L = S.lay[x % kGRing][c];
                 const int32_t pos = L.pos, nu = L.nu;
                 if (pos >= 0) {
                     if (!fetched(x)) break;
 #pragma unroll
                     for (int w = 0; w < (kGMaxU + 5) / 6; ++w) hrow[w] = 0xFFFFFFFFu;  // units past nu: never read
-                    // groups of 4 units (a group past the batch is skipped whole; 4 rather
-                    // than 8: fewer padding units gathered, C2 solver 3.57 -> 3.51 ms)
+                    // groups of 4 units (a group past the batch is skipped whole)
 #pragma unroll
                     for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
                         if (u0 < nu) {
@@ -780,22 +825,22 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 #pragma unroll
                             for (int t = 0; t < 4; ++t) {
                                 uint32_t r8;
-                                ring_get(S, ring_unit(pos, u0 + t), lane, cl[t], vl[t], r8);
+                                ring_get(S, ring_unit(c, pos, u0 + t), lane, cl[t], vl[t], r8);
                                 rw[t] = r8 | gram_pad(u0 + t, nu);
                             }
                             double hx[4];
 #pragma unroll
                             for (int t = 0; t < 4; ++t) {
                                 const int u = u0 + t;
-                                const int32_t c = rw[t] < kGB ? cl[t] : -1;
+                                const int32_t cc = rw[t] < kGB ? cl[t] : -1;
                                 // a hot (LDS) or empty lane loads the constant 1 -- one register
                                 // never mixes a global load with an LDS read (that would serialise)
                                 if (HOTLDS) {
-                                    if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(c >= hot ? dwk + c : &g_gram_one);
-                                    hx[t] = hotl[(c >= 0 && c < hot) ? c : 0];
+                                    if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(cc >= hot ? dwk + cc : &g_gram_one);
+                                    hx[t] = hotl[(cc >= 0 && cc < hot) ? cc : 0];
                                 } else if (!(COCOA_DIAG_ON && (a.diag & 2))) {
                                     // a lane past the batch loads column 0: its product goes to the sink row
-                                    dw[u] = dw_load(dwk + (c >= 0 ? c : 0));
+                                    dw[u] = dw_load(dwk + (cc >= 0 ? cc : 0));
                                 }
                             }
                             __builtin_amdgcn_sched_barrier(0);  // all reads of the group out before the products
@@ -815,7 +860,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     xnu = nu;
                 } else {
                     // too long to stage: gathered and summed here
-                    double* bs = S.base + (x % kGNB) * kGB;
+                    double* bs = S.base[c] + (x % kGNB) * kGB;
                     for (int i = 0; i < kGB; ++i) {
                         const int32_t z = L.sx[i + 1] - L.sx[i];
                         const int64_t rb = L.sb[i];
@@ -825,15 +870,15 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         if (lane == 0) bs[i] = t;
                     }
                     wave_lds_sync();
-                    if (lane == 0) lds_release(&S.cnt[kCBase], x + 1);
+                    if (lane == 0) lds_release(&S.cnt[kCBase + c], x + 1);
                 }
             }
             stamp(2);
         }
         vm_drain();  // the last atomics land before the kernel ends
         if (a.prof && lane == 0)
-            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * 32 + 16 + i] = ph[i];
-    } else if (wv == 0) {
+            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * 32 + 24 + 4 * c + i] = ph[i];
+    } else if (wv == kWChain) {
         // -------------------------------------------------------- chain --
         // lane = window slot (step mod 64): sdot = base + Gram corrections
         const int32_t ahead = MODE != MODE_MBCD ? kGGt + 2 : 0;  // kCLoad needed for batch g: g + 1 + kGNB (records), g + 6 (Gram rows)
@@ -855,19 +900,28 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             const int q4 = g % kGNB;          // this batch's quarter of the lanes
             const bool mine = lane / kGB == q4;
             if (MODE != MODE_MBCD) {
-                if (!wait_ge(&S.cnt[kCBase], g + 1, abortf, a.status, pw)) return false;
+#pragma unroll
+                for (int c = 0; c < kGNC; ++c)
+                    if (!wait_ge(&S.cnt[kCBase + c], g + 1, abortf, a.status, pw)) return false;
                 if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw)) return false;
             } else if (!wait_ge(&S.cnt[kCLoad], min(g + kGNB + 1, NB), abortf, a.status, pw)) {
                 return false;
             }
-            // coefficient ring slot g % kGRing held batch g - kGRing: consumed?
-            if (!wait_ge(&S.cnt[kCScat], g - kGRing + 1, abortf, a.status, pw)) return false;
+            // coefficient ring slot g % kGRing held batch g - kGRing: consumed by both memory waves?
+#pragma unroll
+            for (int c = 0; c < kGNC; ++c)
+                if (!wait_ge(&S.cnt[kCScat + c], g - kGRing + 1, abortf, a.status, pw)) return false;
             {
                 const int32_t g4 = g + kGNB;
                 const GRec& R4 = S.rec[(g4 % kGRing) * kGB + (lane & (kGB - 1))];
                 aissue = alv[(mine && g4 < NB) ? R4.r : nl];  // one load for every lane (the sink otherwise)
             }
-            if (mine) acc += S.base[lane];
+            if (mine) {
+                double bsum = S.base[0][lane];
+#pragma unroll
+                for (int c = 1; c < kGNC; ++c) bsum += S.base[c][lane];
+                acc += bsum;
+            }
             double gcur[kGB];
 #pragma unroll
             for (int i = 0; i < kGB; ++i) gcur[i] = MODE != MODE_MBCD ? S.gring[g % kGGt][i][lane] : 0.0;
@@ -958,8 +1012,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             if (g + 1 < NB && !batch(g + 1, aB, aA)) break;
         }
     }
-    if (a.prof && lane == 0 && wv < 4) {
-        uint64_t* pr = a.prof + (size_t)k * 32 + wv * 4;  // [k][32]: waves 0..3 at 0..15, memory phases at 16..19
+    if (a.prof && lane == 0) {
+        uint64_t* pr = a.prof + (size_t)k * 32 + wv * 4;  // [k][32]: waves 0..5 at 0..23, memory phases at 24..31
         pr[0] = wait_cycles;
         pr[1] = __builtin_readcyclecounter() - t_start;
     }

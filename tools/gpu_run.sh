@@ -52,6 +52,18 @@ for step in "$@"; do
       line c5_localsgd --method localsgd --steps 10 --warmup 2 || exit $?
       line c3 --config c3 --steps 10 --warmup 2 || exit $?
       line c4 --config c4 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+    evalab)  # eval kernel variants (COCOA_EVAL_VARIANT) on the C2 bench
+      for v in ${EVAL_VARIANTS:-0 1 2}; do
+        COCOA_EVAL_VARIANT=$v timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-gap ${BENCH_ARGS} \
+          > $O/evalab_${v}_$TAG.json 2> $O/evalab_${v}_$TAG.err || exit $?
+        python3 -c "import json;d=json.loads(open('$O/evalab_${v}_$TAG.json').readlines()[-1]);print('eval variant $v', round(d['kernel_ms']['eval'],4), 'ms', round(d['roofline_eval']['frac'],3), 'step', round(d['ms_per_step'],3), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
+      done ;;
+    evalpmc)  # PMC counters of the eval kernel (one pass per counter group)
+      for grp in "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "TCC_HIT_sum TCC_MISS_sum" "TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU"; do
+        n=$(echo $grp | cut -d' ' -f1)
+        COCOA_EVAL_VARIANT=${EV:-0} timeout -s KILL 120 rocprofv3 --pmc $grp -d $O/evalpmc_${n}_$TAG -o run --output-format csv -- $SHORT \
+          > $O/evalpmc_${n}_$TAG.log 2>&1 || exit $?
+      done ;;
     gramprof)
       COCOA_LIB=build/diag/libcocoa_hip.so timeout -k 10 200 python3 tools/prof_gram.py cocoa+ \
         > $O/prof_gram_$TAG.json 2> $O/prof_gram_$TAG.err || exit $? ;;
