@@ -8,7 +8,7 @@ BUILD := build/obj
 COMMON := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Iinclude -I$(CSRC)
 HDRS := $(wildcard $(CSRC)/*.h) include/cocoa_capi.h
 
-all: $(OUT) oracle/liboracle.so cocoa_amd/cocoa_driver
+all: $(OUT) oracle/liboracle.so cocoa_amd/cocoa_driver ubench
 
 $(BUILD)/%.strict.o: $(CSRC)/%.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(COMMON) -ffp-contract=off -c $< -o $@
@@ -48,7 +48,12 @@ oracle/liboracle.so: oracle/cocoa_oracle.c
 $(BUILD):
 	mkdir -p $(BUILD)
 
+# PMC calibration / latency micro-benchmarks (tools/gpu_run.sh pmc)
+ubench: tools/ubench/calib tools/ubench/lat
+tools/ubench/%: tools/ubench/%.hip
+	$(HIPCC) -O2 --offload-arch=$(ARCH) $< -o $@
+
 clean:
 	rm -rf build $(OUT) cocoa_amd/cocoa_driver oracle/liboracle.so
 
-.PHONY: all clean diag
+.PHONY: all clean diag ubench

@@ -31,9 +31,11 @@ def pick(agg, needle, counter):
 
 
 def main():
+    # tools/pmc_summary.py [SRC_DIR [TAG]]: TAG = the tools/gpu_run.sh TAG of the passes
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out")
-    f, w = load(os.path.join(src, "pmc_FETCH_SIZE")), load(os.path.join(src, "pmc_WRITE_SIZE"))
-    cf, cw = load(os.path.join(src, "calib_FETCH_SIZE")), load(os.path.join(src, "calib_WRITE_SIZE"))
+    sfx = "_" + sys.argv[2] if len(sys.argv) > 2 else ""
+    f, w = load(os.path.join(src, "pmc_FETCH_SIZE" + sfx)), load(os.path.join(src, "pmc_WRITE_SIZE" + sfx))
+    cf, cw = load(os.path.join(src, "calib_FETCH_SIZE" + sfx)), load(os.path.join(src, "calib_WRITE_SIZE" + sfx))
     gib = float(1 << 30)
     k_f64 = gib / (pick(cf, "read_f64", "FETCH_SIZE")[0] * 1024)
     k_i32 = gib / (pick(cf, "read_i32", "FETCH_SIZE")[0] * 1024)
