@@ -1010,8 +1010,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
     a.scaling = ctx->scaling;
 
-    // the loader of the SDCA solvers is fed by the per-step plan
-    ctx->use_plan = is_sdca(method);
+    // the loader of the SDCA solvers (and of local SGD on the Gram solver) is
+    // fed by the per-step plan; set below, once the solver is chosen
     // fast SDCA: the Gram-window solver, unless the rows are dense-long (C3:
     // 2,000 entries per row, where the chain solver streams w / deltaW from LDS)
     const double zavg = ctx->tr.n ? (double)ctx->tr.nnz / (double)ctx->tr.n : 0.0;
@@ -1033,9 +1033,13 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         ensure_cols(ctx->tr, ctx->d, s);
         a.col = ctx->dw_compact ? ctx->col_local.as<int32_t>() : ctx->tr.col.as<int32_t>();
     }
-    ctx->use_gram = !ctx->strict && !ctx->use_dense && is_sdca(method) && H >= 1 &&
+    // local SGD runs on the Gram solver too (MODE_LSGD, dense slices: its
+    // epilogue reads wInit by the slice's column)
+    const bool gram_method = is_sdca(method) || (method == COCOA_METHOD_LOCALSGD && !ctx->dw_compact);
+    ctx->use_gram = !ctx->strict && !ctx->use_dense && gram_method && H >= 1 &&
                     (ctx->solver_kind == COCOA_SOLVER_GRAM ||
                      (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0 && K <= ncu));
+    ctx->use_plan = is_sdca(method) || ctx->use_gram;
     if (ctx->use_gram) {
         ctx->status.alloc_zero(sizeof(int) * 4, s);
         ctx->nbatch = (H + 15) / 16;  // kGB = 16 steps per batch (solver_gram.h)
@@ -1162,6 +1166,8 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         // (samples, Gram rows) of this round: prefetched during the last round's
         // solver (overlap), else computed here
         const bool gram_rows = c->use_gram && c->method != COCOA_METHOD_MBCD;
+        // SGD.scala:53: t = (t-1) * localIters * parts, an Int product
+        const double lsgd_t0 = (double)wrap32((int64_t)(t - 1) * H * c->K_glob);
         // COCOA_GRAM_SERIAL=1 (diagnostic A/B only): Gram rows in line, before the solver
         static const bool serial = std::getenv("COCOA_GRAM_SERIAL") && std::atoi(std::getenv("COCOA_GRAM_SERIAL"));
         const bool overlap = gram_rows && c->gstream && c->gt2.p && !serial;
@@ -1232,7 +1238,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.scaling = c->scaling;
             g.proj = c->proj_rule() ? 1 : 0;
             c->timed(COCOA_K_SOLVER, [&] { launch_solver_dense(solver_mode(c->method), g, K, c->max_nl, s); });
-        } else if (c->use_gram) {
+        } else if (c->use_gram && (c->method != COCOA_METHOD_LOCALSGD || lsgd_t0 >= 0)) {
             GramSolverArgs g{};
             g.part_ptr = c->part_ptr.as<int64_t>();
             g.samples = smp;
@@ -1259,7 +1265,11 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.sigma = c->method == COCOA_METHOD_COCOA_PLUS ? c->sa.sigma : 1.0;
             g.scaling = c->scaling;
             g.proj = c->proj_rule() ? 1 : 0;
-            c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(solver_mode(c->method), g, K, s); });
+            g.w = c->w.as<double>();
+            g.lambda = c->P.lambda;
+            g.t0 = lsgd_t0;
+            const int mode = c->method == COCOA_METHOD_LOCALSGD ? MODE_LSGD : solver_mode(c->method);
+            c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(mode, g, K, s); });
             if (overlap) {
                 // round t+1's samples and Gram rows on gstream, beside this solver (its
                 // buffer's last reader, round t-1's solver, is done first)
@@ -1296,7 +1306,10 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
                 c->timed(COCOA_K_APPLY, [&] { launch_scale(c->w.as<double>(), d, scale, s); });
                 c->mult = step * c->scaling;                                 // SGD.scala:58
             }
-            const double t0 = (double)wrap32((int64_t)(t - 1) * H * c->K_glob); // SGD.scala:53 (Int)
+            // (local SGD lands here on the strict path, or in the fast path for a
+            // round whose Int step counter wrapped negative: its shrink sequence can
+            // pass through 0 or blow up, which the Gram solver's scalar s does not model)
+            const double t0 = lsgd_t0;
             c->timed(COCOA_K_SOLVER, [&] {
                 if (c->strict)
                     launch_sgd(local, c->sa, c->P.lambda, t0, K, s);

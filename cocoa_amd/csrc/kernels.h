@@ -10,7 +10,8 @@
 
 namespace cocoa {
 
-enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2 };
+// MODE_LSGD: local SGD (SGD.scala:87-139, local = true) on the Gram-window solver
+enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2, MODE_LSGD = 3 };
 
 constexpr int kWave = 64;
 constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
@@ -143,6 +144,10 @@ struct GramSolverArgs {
     double lam_n, inv_lam_n;
     double sigma;             // sigma' = K gamma (CoCoA+)
     double scaling;
+    // MODE_LSGD: step_i = 1 / (lambda (t0 + i)) (SGD.scala:106); w = wInit, the
+    // epilogue turns the slice's delta-v into deltaW = s (keep wInit + dv) - wInit
+    const double* w;
+    double lambda, t0;
 };
 
 // Dense-row local solver (solver_dense.h), fast mode: X is the CSR value array

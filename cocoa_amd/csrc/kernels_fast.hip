@@ -81,12 +81,14 @@ void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t
         g.hot = 0;
         if (mode == MODE_PLUS) launch_sg<MODE_PLUS, false>(g, grid, lds, s);
         else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, false>(g, grid, lds, s);
+        else if (mode == MODE_LSGD) launch_sg3<MODE_LSGD, false, false>(g, grid, lds, s);
         else launch_sg<MODE_MBCD, false>(g, grid, lds, s);
         return;
     }
 #ifdef COCOA_DIAG
     if (mode == MODE_PLUS) launch_sg<MODE_PLUS, true>(g, grid, lds, s);
     else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, true>(g, grid, lds, s);
+    else if (mode == MODE_LSGD) launch_sg3<MODE_LSGD, true, false>(g, grid, lds, s);
     else launch_sg<MODE_MBCD, true>(g, grid, lds, s);
 #endif
 }

@@ -50,6 +50,17 @@
 // results agree with the strict path / oracle within the north_star
 // tolerance.  MbCD reads the stale w only (MinibatchCD.scala:104): no base,
 // no Gram term, the chain is the update rule alone.
+//
+// Local SGD (MODE_LSGD, SGD.scala:87-139 with local = true) runs on the same
+// machinery.  The reference shrinks its whole w copy every step (w *= 1 -
+// step lambda, SGD.scala:119-120); here w = s (keep wInit + v), with the
+// shrink in the scalar s and v = sum of u_j x_j, u_j = y_j step_j / s_j for the
+// violators j (SGD.scala:124-129).  s depends only on the step index (t0 + i),
+// so the loader forms it (and the step's constants) ahead of the chain, and
+//   x_s . w_s = s_{s-1} (keep x_s.wInit + base_s + sum_j u_j G(s, j))
+// with the same base / Gram split as above (the slice holds v).  A shrink of
+// exactly 0 (step 1 of round 1) drops wInit: keep = 0, s = 1.  The epilogue
+// writes deltaW = w - wInit = s keep wInit + s v - wInit (SGD.scala:133).
 #pragma once
 #include "kernels.h"
 #include "wave.h"
@@ -432,6 +443,8 @@ static_assert(kCFetch + kGNC <= 16, "counters");
 
 struct GramSolverLds {
     int cnt[16];
+    double lsgd_s;                     // MODE_LSGD: s after the last step (loader -> epilogue)
+    int32_t lsgd_keep, lsgd_pad;       //   and whether wInit survived (no zero shrink)
     GRec rec[kGRing * kGB];            // ring: (b % kGRing) * kGB + i
     double coef[kGRing * 2 * kGB];     // c_j, same ring (chain -> memory waves); [kGB, 2 kGB) of a slot stay 0
     GLay lay[kGRing][kGNC];            // same ring (loader -> fetch / memory waves)
@@ -537,8 +550,10 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     const double* gt = a.gt + (size_t)k * a.nbatch * kGB * kGSlots;
     int* abortf = &S.cnt[kCAbort];
 
-    for (int32_t i = tid; i < nl; i += kGThreads) alv[i] = a.alpha[p0 + i];
-    if (tid == 0) alv[nl] = 0.0;
+    if (MODE != MODE_LSGD) {
+        for (int32_t i = tid; i < nl; i += kGThreads) alv[i] = a.alpha[p0 + i];
+        if (tid == 0) alv[nl] = 0.0;
+    }
     for (int i = tid; i < kGNC * kGSlots; i += kGThreads) (&S.base[0][0])[i] = 0.0;  // batches 0 .. kGNB-1
     for (int32_t i = tid; i < hot; i += kGThreads) hotl[i] = 0.0;
     for (int i = tid; i < kGRing * 2 * kGB; i += kGThreads) S.coef[i] = 0.0;  // zero slots: rows past a batch
@@ -561,6 +576,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         int32_t xr = nl, xz = 0, xz0 = 0;
         double xy = 0.0, xq = 0.0, xxw = 0.0;
         int64_t xbeg = 0;
+        double ls = 1.0;   // MODE_LSGD: s before the batch (SGD.scala:119-120), wave-uniform
+        int32_t lkeep = 1; //   wInit not yet dropped by a zero shrink
         auto load = [&](int32_t b) {
             const int32_t j = b * kGB + i;
             xr = nl;
@@ -600,7 +617,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 const int64_t beg = xbeg;
                 if (b + 1 < NB) load(b + 1);
                 const int32_t w0 = b * kGB - kGSlots;  // look-back window: steps [w0, w0 + kGWin)
-                if (lane < kGB) S.smpwin[j & (2 * kGSlots - 1)] = valid ? r : -2;
+                if (MODE != MODE_LSGD && lane < kGB) S.smpwin[j & (2 * kGSlots - 1)] = valid ? r : -2;
                 // the rows' runs of each class: class 0 = entries [beg, beg + z0), class 1 = the rest
                 int32_t inc[kGNC], T[kGNC], nu[kGNC];
 #pragma unroll
@@ -614,7 +631,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 // previous occurrence of each step's row in the window before it: lanes =
                 // window positions (0..63: batches b-4 .. b-1; 64 + lane: this batch)
                 int32_t pd = -1;
-                {
+                if (MODE != MODE_LSGD) {  // (no dual variable to forward in local SGD)
                     const int32_t ra = S.smpwin[(w0 + lane) & (2 * kGSlots - 1)];
                     const int32_t rb = valid ? r : -3;
                     const int32_t m = min(kGB, H - b * kGB);
@@ -626,10 +643,45 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         if (lane == t) pd = p;
                     }
                 }
+                // MODE_LSGD: the step's shrink and s, in step order (SGD.scala:106, 119-120)
+                // on the uniform running s, so every partition forms the same sequence
+                double lB = 0.0, lAE = 0.0, lY = 0.0;
+                if (MODE == MODE_LSGD) {
+                    const double step = valid ? 1.0 / (a.lambda * (a.t0 + (double)(j + 1))) : 0.0;
+                    const double scale = valid ? 1.0 - step * a.lambda : 1.0;
+                    double sprev = 1.0, snew = 1.0;
+                    int32_t kprev = 1;
+                    for (int t = 0; t < kGB; ++t) {
+                        const double sc = readlane_d(scale, t);
+                        if (lane == t) {
+                            sprev = ls;
+                            kprev = lkeep;
+                        }
+                        if (sc == 0.0) {  // w *= 0: wInit and v dropped, s restarts
+                            ls = 1.0;
+                            lkeep = 0;
+                        } else {
+                            ls *= sc;
+                        }
+                        if (lane == t) snew = ls;
+                    }
+                    // eval = 1 - y x.w = AE - B (base + corrections); violators scatter
+                    // u = y step / s (SGD.scala:115, 124-129)
+                    lB = valid ? y * sprev : 0.0;
+                    lAE = valid ? 1.0 - lB * (kprev ? xw : 0.0) : 0.0;
+                    lY = valid ? (y * step) / snew : 0.0;
+                }
                 if (lane < kGB) {
                     GRec& R = S.rec[(b % kGRing) * kGB + lane];
                     double B = 0.0, E = 0.0, Y = 0.0;
-                    if (valid) gram_row_consts<MODE>(a, y, q, xw, B, E, Y);
+                    if (MODE == MODE_LSGD) {
+                        B = lB;
+                        Y = lY;
+                        R.AE = lAE;
+                        R.YA = 0.0;
+                    } else if (valid) {
+                        gram_row_consts<MODE>(a, y, q, xw, B, E, Y);
+                    }
                     R.B = B;
                     R.E = E;
                     R.Y = Y;
@@ -654,7 +706,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 }
                 wave_lds_sync();
                 // mark the earlier occurrence: step w0 + pd forwards its new alpha here
-                if (lane < kGB && pd >= 0) {
+                if (MODE != MODE_LSGD && lane < kGB && pd >= 0) {
                     const int32_t js = w0 + pd;
                     S.rec[((js / kGB) % kGRing) * kGB + (js % kGB)].fw = j & (2 * kGSlots - 1);
                 }
@@ -668,6 +720,10 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             }
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCLoad], b + 1);
+        }
+        if (MODE == MODE_LSGD && lane == 0) {  // read after the final barrier
+            S.lsgd_s = ls;
+            S.lsgd_keep = lkeep;
         }
     } else if (wv == kWFetch0 || wv == kWFetch1) {
         // -------------------------------------------------------- fetch --
@@ -884,7 +940,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         const int32_t ahead = MODE != MODE_MBCD ? kGGt + 2 : 0;  // kCLoad needed for batch g: g + 1 + kGNB (records), g + 6 (Gram rows)
         bool ok = wait_ge(&S.cnt[kCLoad], MODE != MODE_MBCD ? ahead : min(kGNB + 1, NB), abortf, a.status, pw);
         double acc = 0.0;
-        if (ok && lane / kGB < NB) {
+        if (MODE != MODE_LSGD && ok && lane / kGB < NB) {  // (local SGD: the loader sets AE)
             GRec& R = S.rec[(lane / kGB) * kGB + (lane & (kGB - 1))];
             const double aa = alv[R.r];
             R.AE = aa - R.E;
@@ -911,7 +967,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 #pragma unroll
             for (int c = 0; c < kGNC; ++c)
                 if (!wait_ge(&S.cnt[kCScat + c], g - kGRing + 1, abortf, a.status, pw)) return false;
-            {
+            if (MODE != MODE_LSGD) {
                 const int32_t g4 = g + kGNB;
                 const GRec& R4 = S.rec[(g4 % kGRing) * kGB + (lane & (kGB - 1))];
                 aissue = alv[(mine && g4 < NB) ? R4.r : nl];  // one load for every lane (the sink otherwise)
@@ -952,6 +1008,13 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             // once at the end for the alpha and coefficient stores.
 #pragma unroll
             for (int i = 0; i < kGB; ++i) {
+                if (MODE == MODE_LSGD) {
+                    // SGD.scala:115, 124-129: eval = 1 - y x.w > 0 scatters u = y step / s
+                    const double ev = fma(-rB, acc, rAE);
+                    const double cf = readlane_d(ev > 0.0 ? rY : 0.0, slot0 + i);
+                    acc = fma(cf, gcur[i], acc);
+                    continue;
+                }
                 // CoCoA.scala:159-186 / MinibatchCD.scala:104-123 (see above)
                 const double nt = gram_rule<PROJ>(fma(-rB, acc, rAE), rAA);
                 if (MODE != MODE_MBCD) {
@@ -980,7 +1043,10 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     }
                 }
             }
-            {
+            if (MODE == MODE_LSGD) {
+                const double ev = fma(-rB, acc, rAE);
+                if (mine) cfo[lane & (kGB - 1)] = ev > 0.0 ? rY : 0.0;
+            } else {
                 const double nt = gram_rule<PROJ>(fma(-rB, acc, rAE), rAA);
                 const double cf = fma(rY, nt, -rYA);
                 if (mine) {
@@ -995,7 +1061,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             // alpha of batch g+3 (loaded at the start of batch g-1 by the previous
             // quarter), unless a forward already set it
             const int32_t g3 = g + kGNB - 1;
-            if (g >= 1 && g3 < NB && lane / kGB == (g + kGNB - 1) % kGNB) {
+            if (MODE != MODE_LSGD && g >= 1 && g3 < NB && lane / kGB == (g + kGNB - 1) % kGNB) {
                 GRec& R3 = S.rec[(g3 % kGRing) * kGB + (lane & (kGB - 1))];
                 if (!R3.fwd) {
                     R3.AE = afill - R3.E;
@@ -1018,6 +1084,16 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         pr[1] = __builtin_readcyclecounter() - t_start;
     }
     __syncthreads();
+    if (MODE == MODE_LSGD) {
+        // deltaW = w - wInit = s (keep wInit + v) - wInit (SGD.scala:133), the slice
+        // holding v (L2: read past L1, like the gathers)
+        const double sH = S.lsgd_s, f = S.lsgd_keep ? sH - 1.0 : -1.0;
+        for (int64_t j = tid; j < a.d; j += kGThreads) {
+            const double v = (HOTLDS && j < hot) ? hotl[j] : dw_load(dwk + j);
+            dwk[j] = fma(sH, v, f * a.w[j]);
+        }
+        return;
+    }
     for (int32_t i = tid; i < hot; i += kGThreads) dwk[i] = hotl[i];  // the slice is zero there: plain stores
     // alpha = alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101, MinibatchCD.scala:127-128)
     if (a.raw_alpha) {

@@ -137,6 +137,24 @@ def test_c5_sgd_strict_vs_oracle_and_fast(c2, method):
     assert_state_close(f, run, False)
 
 
+def test_c5_localsgd_fast_gram_solver_vs_oracle(c2):
+    """The C5 local-SGD line: the Gram-window solver (MODE_LSGD: w = s (wInit +
+    v), the shrink in the scalar s, x.v split into base + Gram corrections) for 6
+    rounds -- round 1 has the zero shrink of step 1 -- against the oracle's
+    step-by-step SGD.scala restatement."""
+    sh, od, ot = c2
+    e = make_engine(sh, strict=False)
+    e.init("localsgd", sh.n_glob, 6, sh.H, sh.lam)
+    assert e.plan()["solver"] == "gram"
+    run = make_run(sh, od, "localsgd")
+    for t in range(1, 7):
+        e.round(t)
+        run.round(t)
+        if t % 2 == 0:
+            assert_close(e.eval(), run.eval(ot), False, t)
+    assert_state_close(e, run, False)
+
+
 # ------------------------------------------------------------------ C3 --
 @pytest.fixture(scope="module")
 def c3():

@@ -398,6 +398,26 @@ def test_c2_fast_sgd_matches_strict(c2, method):
     assert abs(es["primal"] - ef["primal"]) <= REL * es["primal"]
 
 
+@pytest.mark.parametrize("t", [1, 2, 3579141])
+def test_localsgd_fast_step_counter_rounds(t):
+    """Local SGD's step counter t0 = (t-1) H K is a Scala Int (SGD.scala:53):
+    round 1 (t0 = 0, a zero shrink at step 1), round 2, and a round whose counter
+    wrapped negative (the engine hands that round to the per-step kernel), each
+    from a fresh w = 0 against the oracle."""
+    tr = _dataset_with_edges(5)
+    od = odata(tr)
+    H = 150
+    assert t < 10 or (t - 1) * H * 4 >= 2**31  # t = 3579141: the Int counter wraps
+    run = oracle.Run(od, "localsgd", tr.n, H, 2e-3, seed=2)
+    e = engine(tr, strict=False)
+    e.init("localsgd", tr.n, t, H, 2e-3, 1.0, 1.0, 1, 2)
+    assert e.plan()["solver"] == "gram"
+    run.round(t)
+    e.round(t)
+    wr = run.w()
+    assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+
+
 def test_checkpoint_resume_is_bitwise(c1, tmp_path):
     """Stop after round 3, resume from the (t, w, alpha) checkpoint in a fresh
     context: rounds 4..6 land on exactly the uninterrupted run's w and alpha."""
