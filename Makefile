@@ -31,15 +31,15 @@ $(OUT): $(OBJS)
 cocoa_amd/cocoa_driver: $(CSRC)/driver_main.cpp $(CSRC)/jdouble.h $(OUT) include/cocoa_capi.h
 	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude -I$(CSRC) -x c++ $< -o $@ -Lcocoa_amd -lcocoa_hip -Wl,-rpath,'$$ORIGIN'
 
-# diagnostic build with per-step phase stamps in the local solver
+# diagnostic build with per-step phase stamps in the local solver (always
+# rebuilt; DEFS="-DFOO" adds defines, e.g. an A/B variant's)
 DIAG := build/diag
-diag: $(DIAG)/libcocoa_hip.so
-$(DIAG)/libcocoa_hip.so: $(CSRC)/*.hip $(CSRC)/*.cpp $(HDRS)
+diag:
 	mkdir -p $(DIAG)
-	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -ffp-contract=off -c $(CSRC)/kernels_strict.hip -o $(DIAG)/ks.o
-	$(HIPCC) $(COMMON) -DCOCOA_STEP_PROF -DCOCOA_DIAG -ffp-contract=fast -munsafe-fp-atomics -c $(CSRC)/kernels_fast.hip -o $(DIAG)/kf.o
-	$(HIPCC) $(COMMON) -DCOCOA_DIAG -ffp-contract=off -c $(CSRC)/engine.hip -o $(DIAG)/en.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(DIAG)/ks.o $(DIAG)/kf.o $(DIAG)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o \
+	$(HIPCC) $(COMMON) $(DEFS) -DCOCOA_STEP_PROF -ffp-contract=off -c $(CSRC)/kernels_strict.hip -o $(DIAG)/ks.o
+	$(HIPCC) $(COMMON) $(DEFS) -DCOCOA_STEP_PROF -DCOCOA_DIAG -ffp-contract=fast -munsafe-fp-atomics -c $(CSRC)/kernels_fast.hip -o $(DIAG)/kf.o
+	$(HIPCC) $(COMMON) $(DEFS) -DCOCOA_DIAG -ffp-contract=off -c $(CSRC)/engine.hip -o $(DIAG)/en.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(DIAG)/libcocoa_hip.so $(DIAG)/ks.o $(DIAG)/kf.o $(DIAG)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o \
 	    $(BUILD)/ingest.strict.o -lpthread -ldl
 
 oracle/liboracle.so: oracle/cocoa_oracle.c
@@ -48,12 +48,22 @@ oracle/liboracle.so: oracle/cocoa_oracle.c
 $(BUILD):
 	mkdir -p $(BUILD)
 
+# A/B variant of the library: make variant V=name DEFS="-DFOO=1" -> build/v_name/libcocoa_hip.so
+# (COCOA_LIB=build/v_name/libcocoa_hip.so selects it; tools/gpu_run.sh ab)
+variant:
+	mkdir -p build/v_$(V)
+	$(HIPCC) $(COMMON) $(DEFS) -ffp-contract=off -c $(CSRC)/kernels_strict.hip -o build/v_$(V)/ks.o
+	$(HIPCC) $(COMMON) $(DEFS) -ffp-contract=fast -munsafe-fp-atomics -c $(CSRC)/kernels_fast.hip -o build/v_$(V)/kf.o
+	$(HIPCC) $(COMMON) $(DEFS) -ffp-contract=off -c $(CSRC)/engine.hip -o build/v_$(V)/en.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o build/v_$(V)/libcocoa_hip.so build/v_$(V)/ks.o build/v_$(V)/kf.o \
+	    build/v_$(V)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o $(BUILD)/ingest.strict.o -lpthread -ldl
+
 # PMC calibration / latency micro-benchmarks (tools/gpu_run.sh pmc)
-ubench: tools/ubench/calib tools/ubench/lat
+ubench: tools/ubench/calib tools/ubench/lat tools/ubench/ldsdma
 tools/ubench/%: tools/ubench/%.hip
 	$(HIPCC) -O2 --offload-arch=$(ARCH) $< -o $@
 
 clean:
 	rm -rf build $(OUT) cocoa_amd/cocoa_driver oracle/liboracle.so
 
-.PHONY: all clean diag ubench
+.PHONY: all clean diag ubench variant

@@ -74,8 +74,13 @@
 namespace cocoa {
 
 constexpr int kGB = 16;                  // steps per batch
-constexpr int kGSlots = 64;              // window slots = lanes
-constexpr int kGNB = kGSlots / kGB;      // batches in the window
+constexpr int kGSlots = 64;              // lanes; Gram-row stride (doubles)
+#ifndef COCOA_GWIN
+#define COCOA_GWIN 64
+#endif
+constexpr int kGW = COCOA_GWIN;          // window slots (steps): slot of step s = s mod kGW
+constexpr int kGNB = kGW / kGB;          // batches in the window
+static_assert(kGW % kGB == 0 && kGW <= kGSlots && kGNB >= 2, "window");
 constexpr int kGRing = 8;                // record / coefficient ring (batches)
 constexpr int kGHot = 32;                // dense hot columns of gram_kernel (device order: most frequent first)
 
@@ -191,7 +196,7 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
     }
     const int32_t H = a.H;
     const int32_t j0 = g * kGB;
-    const int32_t P = min(kGSlots, H - j0);     // partners [j0, j0 + P)
+    const int32_t P = min(kGW, H - j0);         // partners [j0, j0 + P)
     const int32_t U = min(kGB, H - j0);          // updaters = partners [0, U)
     const int64_t p0 = a.part_ptr[k];
     const int32_t* smp = a.samples + (size_t)k * H;
@@ -367,11 +372,13 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
     }
     __syncthreads();
     phase(3);
-    // Gt rows of the block's updaters: slot of partner p = (j0 + p) & 63
+    // Gt rows of the block's updaters: slot of partner p = (j0 + p) mod kGW (slots
+    // past the window: zero)
     double* out = a.gt + ((size_t)k * a.nbatch * kGB + j0) * kGSlots;
+    const int slot = lane < kGW ? ((g % kGNB) * kGB + lane) % kGW : lane;
     for (int u = wv; u < kGB; u += kGramThreads / 64) {
         const double v = (u < U && lane > u && lane < P) ? L.acc[u][lane] : 0.0;
-        __builtin_nontemporal_store(v, out + (size_t)u * kGSlots + ((j0 + lane) & (kGSlots - 1)));
+        __builtin_nontemporal_store(v, out + (size_t)u * kGSlots + slot);
     }
     phase(4);
 }
@@ -403,7 +410,7 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
 // inside one wave's address stream, and the two memory waves -- the issue-
 // bound part of the round -- run on different SIMDs.  The chain adds the two
 // partial bases.
-constexpr int kGWin = kGSlots + kGB;     // loader's look-back for alpha forwarding: 5 batches
+constexpr int kGWin = kGW + kGB;         // loader's look-back for alpha forwarding: the window + 1 batch
 constexpr int kGNC = 2;                  // column classes = memory waves = fetch waves
 constexpr int kGE = 8192;                // staged entries (LDS ring positions), all classes
 constexpr int kGSub = kGE / 64 / kGNC;   // 64-entry units of one class's sub-ring
@@ -488,9 +495,15 @@ __device__ __forceinline__ int gram_owner(const int32_t* excl, int32_t q) {
     return lo;
 }
 
-// 4 bytes per lane from global memory straight into LDS (lds + 4 * lane)
+// 4 bytes per lane from global memory straight into LDS (lds + 4 * lane).
+// Cache policy of the streams read once per round (CSR entries of the sampled
+// rows, Gram rows): COCOA_GRAM_NT = 2 marks them nt (MI355X_MICROARCH.md
+// nt-weights), so they pass L2 without evicting the deltaW slices.
+#ifndef COCOA_GRAM_NT
+#define COCOA_GRAM_NT 0
+#endif
 __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, COCOA_GRAM_NT);
 }
 
 // 0 for a unit of the batch (u < nu), 0xFF (row: no entry) past it.  The row byte is
@@ -616,7 +629,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 const double y = xy, q = xq, xw = xxw;
                 const int64_t beg = xbeg;
                 if (b + 1 < NB) load(b + 1);
-                const int32_t w0 = b * kGB - kGSlots;  // look-back window: steps [w0, w0 + kGWin)
+                const int32_t w0 = b * kGB - kGW;  // look-back window: steps [w0, w0 + kGWin)
                 if (MODE != MODE_LSGD && lane < kGB) S.smpwin[j & (2 * kGSlots - 1)] = valid ? r : -2;
                 // the rows' runs of each class: class 0 = entries [beg, beg + z0), class 1 = the rest
                 int32_t inc[kGNC], T[kGNC], nu[kGNC];
@@ -629,17 +642,17 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 }
                 wave_lds_sync();
                 // previous occurrence of each step's row in the window before it: lanes =
-                // window positions (0..63: batches b-4 .. b-1; 64 + lane: this batch)
+                // window positions (0..kGW-1: batches b-kGNB .. b-1; kGW + lane: this batch)
                 int32_t pd = -1;
                 if (MODE != MODE_LSGD) {  // (no dual variable to forward in local SGD)
-                    const int32_t ra = S.smpwin[(w0 + lane) & (2 * kGSlots - 1)];
+                    const int32_t ra = lane < kGW ? S.smpwin[(w0 + lane) & (2 * kGSlots - 1)] : -4;
                     const int32_t rb = valid ? r : -3;
                     const int32_t m = min(kGB, H - b * kGB);
                     for (int t = 0; t < m; ++t) {
                         const int32_t rt = __builtin_amdgcn_readlane(r, t);
                         const uint64_t mb = __ballot(rb == rt && lane < t);
                         const uint64_t ma = __ballot(ra == rt);
-                        const int32_t p = mb ? kGSlots + 63 - __builtin_clzll(mb) : (ma ? 63 - __builtin_clzll(ma) : -1);
+                        const int32_t p = mb ? kGW + 63 - __builtin_clzll(mb) : (ma ? 63 - __builtin_clzll(ma) : -1);
                         if (lane == t) pd = p;
                     }
                 }
@@ -728,6 +741,72 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     } else if (wv == kWFetch0 || wv == kWFetch1) {
         // -------------------------------------------------------- fetch --
         const int c = wv == kWFetch0 ? 0 : 1;
+#ifdef COCOA_FETCH2
+        // Per batch: the entry offsets of all its units first (owners by four
+        // interleaved binary searches), then the previous batch's DMA is drained and
+        // published, then this batch's DMA goes out: the DMA latency of batch x-1
+        // hides behind batch x's address work instead of ending every batch.  The
+        // ring-space wait for batch x comes after batch x-1 is published (the memory
+        // waves free space only after consuming it: no cycle through the wait).
+        int32_t prev = -1;
+        for (int32_t x = 0; x < NB; ++x) {
+            if (!wait_ge(&S.cnt[kCLoad], x + 1, abortf, a.status, pw)) break;
+            const GLay& L = S.lay[x % kGRing][c];
+            const int32_t pos = L.pos, nu = L.nu, T = L.T;
+            const bool staged = pos >= 0 && nu > 0;
+            int64_t ee[kGMaxU];
+            uint32_t ro[kGMaxU];
+            if (staged) {
+#pragma unroll
+                for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
+                    if (u0 < nu) {
+                        int o[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) o[t] = 0;
+#pragma unroll
+                        for (int st = kGB / 2; st >= 1; st >>= 1) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                if (L.sx[o[t] + st] <= (u0 + t) * 64 + lane) o[t] += st;
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int32_t q = (u0 + t) * 64 + lane;
+                            ee[u0 + t] = L.sb[o[t]] + (q - L.sx[o[t]]);
+                            ro[u0 + t] = (q < T) ? (uint32_t)o[t] : 0xFFu;
+                        }
+                    }
+                }
+            }
+            if (prev >= 0) {
+                vm_drain();  // batch prev's DMA writes are in LDS
+                wave_lds_sync();
+                if (lane == 0) lds_release(&S.cnt[kCFetch + c], prev + 1);
+            }
+            if (staged && !wait_ge(&S.cnt[kCFreed + c], pos + nu * 64 - kGSub * 64, abortf, a.status, pw)) break;
+            if (staged) {
+#pragma unroll
+                for (int u = 0; u < kGMaxU; ++u) {
+                    if (u < nu) {
+                        uint8_t* ub = S.ring[ring_unit(c, pos, u)];
+                        if (ro[u] != 0xFFu) {
+                            const int64_t e = ee[u];
+                            lds_dma4(a.col + e, ub + kGOCol);
+                            lds_dma4((const uint32_t*)(a.val + e), ub + kGOLo);
+                            lds_dma4((const uint32_t*)(a.val + e) + 1, ub + kGOHi);
+                        }
+                        ub[kGORow + lane] = (uint8_t)ro[u];
+                    }
+                }
+            }
+            prev = x;
+        }
+        if (prev >= 0) {
+            vm_drain();
+            wave_lds_sync();
+            if (lane == 0) lds_release(&S.cnt[kCFetch + c], prev + 1);
+        }
+#else
         for (int32_t x = 0; x < NB; ++x) {
             if (!wait_ge(&S.cnt[kCLoad], x + 1, abortf, a.status, pw)) break;
             const GLay& L = S.lay[x % kGRing][c];
@@ -752,6 +831,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCFetch + c], x + 1);
         }
+#endif
     } else if (wv == kWMem0 || wv == kWMem1) {
         // ------------------------------------------------------- memory --
         const int c = wv == kWMem0 ? 0 : 1;  // this wave's column class
@@ -779,6 +859,96 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         for (int32_t b = 0; b < NB; ++b) {
             if (!wait_ge(&S.cnt[kCChain], b + 1, abortf, a.status, pw)) break;  // the chain finished batch b
             if (a.prof) tph = __builtin_readcyclecounter();
+#ifdef COCOA_MEM2
+            // Scatter of batch b first, its LDS reads before the drain: the ring entries
+            // and coefficients of b are read into registers while the gathers of batch
+            // b+3 are still in flight; the drain then only orders those gathers before
+            // b's atomics (the per-column order of the slice), and the products of b+3
+            // are formed behind the atomics.
+            {
+                const GLay& L = S.lay[b % kGRing][c];
+                const double* cf = S.coef + (b % kGRing) * (2 * kGB);
+                const int32_t pos = L.pos, nu = L.nu;
+                int32_t scl[kGMaxU];
+                double sp[kGMaxU];
+                if (pos >= 0) {
+                    if (!fetched(b)) break;
+#pragma unroll
+                    for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
+                        if (u0 < nu) {
+                            int rw[4];
+                            double vl[4];
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                uint32_t r8;
+                                ring_get(S, ring_unit(c, pos, u0 + t), lane, scl[u0 + t], vl[t], r8);
+                                rw[t] = r8 | gram_pad(u0 + t, nu);
+                            }
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                // a lane past the batch (row 0xFF) reads a zero slot; its ring
+                                // entry was never written, so it is dropped by the coefficient
+                                const double cc = cf[rw[t] & (2 * kGB - 1)];
+                                sp[u0 + t] = vl[t] * cc;
+                                if (cc == 0.0) scl[u0 + t] = -1;
+                            }
+                        }
+                    }
+                }
+                stamp(3);
+                vm_drain();  // the gathers of batch b+3 have read the slice
+                stamp(0);
+                if (pos >= 0) {
+#pragma unroll
+                    for (int u = 0; u < kGMaxU; ++u)
+                        if (u < nu && scl[u] >= 0 && !(COCOA_DIAG_ON && (a.diag & 1))) dw_add(scl[u], sp[u]);
+                } else {
+                    for (int i = 0; i < kGB; ++i) {
+                        const double cv = cf[i];
+                        if (cv == 0.0) continue;
+                        const int32_t z = L.sx[i + 1] - L.sx[i];
+                        const int64_t rb = L.sb[i];
+                        for (int32_t e = lane; e < z; e += 64) dw_add(a.col[rb + e], a.val[rb + e] * cv);
+                    }
+                }
+                wave_lds_sync();
+                if (lane == 0) {
+                    lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
+                    if (pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                }
+            }
+            // 1. products of the gathers in flight -> this class's part of the base of
+            //    batch xin.  Each unit's product goes to (its row, lane mod 32) with a
+            //    fire-and-forget LDS add (lanes l and l + 32 share a slot: different
+            //    LDS lane groups, no conflict); 4 lanes per row add the slots up.
+            if (xin >= 0) {
+                if (lane < kGPart) {
+#pragma unroll
+                    for (int i = 0; i < kGB; ++i) part[i][lane] = 0.0;
+                }
+                wave_lds_sync();
+#pragma unroll
+                for (int u = 0; u < kGMaxU; ++u) {
+                    if (u < xnu) {
+                        const int row = min((int)((hrow[u / 6] >> (5 * (u % 6))) & 31u), kGB);  // 31: no entry
+                        __hip_atomic_fetch_add(&part[row][lane & (kGPart - 1)], hv[u] * dw[u], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                wave_lds_sync();
+                const int rr = lane >> 2, qq = (lane & 3) * (kGPart / 4);
+                double s4 = 0.0;
+#pragma unroll
+                for (int t = 0; t < kGPart / 4; ++t) s4 += part[rr][qq + t];
+                s4 += dpp_row_d<0xB1>(s4);  // quad_perm [1,0,3,2]
+                s4 += dpp_row_d<0x4E>(s4);  // quad_perm [2,3,0,1]
+                if ((lane & 3) == 0) S.base[c][(xin % kGNB) * kGB + rr] = s4;
+                wave_lds_sync();
+                if (lane == 0) lds_release(&S.cnt[kCBase + c], xin + 1);
+                xin = -1;
+            }
+            stamp(1);
+#else
             // every load of the previous iteration has landed (step 1 needs the gathers
             // anyway): the compiler then knows no register is still being written and
             // issues step 3's loads back to back instead of waiting before each one
@@ -860,6 +1030,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 }
             }
             stamp(1);
+#endif
             // 3. gathers of batch x = b + kGNB on this class's columns: they see batch
             //    b's updates (issued above, same wave, same addresses) and nothing later
             //    (the next atomics go out after step 1 has consumed these loads)
@@ -940,7 +1111,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         const int32_t ahead = MODE != MODE_MBCD ? kGGt + 2 : 0;  // kCLoad needed for batch g: g + 1 + kGNB (records), g + 6 (Gram rows)
         bool ok = wait_ge(&S.cnt[kCLoad], MODE != MODE_MBCD ? ahead : min(kGNB + 1, NB), abortf, a.status, pw);
         double acc = 0.0;
-        if (MODE != MODE_LSGD && ok && lane / kGB < NB) {  // (local SGD: the loader sets AE)
+        if (MODE != MODE_LSGD && ok && lane < kGW && lane / kGB < NB) {  // (local SGD: the loader sets AE)
             GRec& R = S.rec[(lane / kGB) * kGB + (lane & (kGB - 1))];
             const double aa = alv[R.r];
             R.AE = aa - R.E;

@@ -8,6 +8,7 @@
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (+ calibration) of the same bench
 #   lines            the C5 / C3 / C4 config lines
 #   gramprof         Gram-solver wave profile (diag build, tools/prof_gram.py)
+#   ab               the short bench on each library in VARIANTS (names of build/v_NAME; "base" = in-tree)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -64,9 +65,23 @@ for step in "$@"; do
         COCOA_EVAL_VARIANT=${EV:-0} timeout -s KILL 120 rocprofv3 --pmc $grp -d $O/evalpmc_${n}_$TAG -o run --output-format csv -- $SHORT \
           > $O/evalpmc_${n}_$TAG.log 2>&1 || exit $?
       done ;;
+    solverpmc)  # PMC groups of the solver / gram kernels (one pass per group; PMC_LIB selects a variant)
+      for grp in "TA_BUSY_avr TA_BUSY_max" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU" "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAVES GRBM_GUI_ACTIVE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL"; do
+        n=$(echo $grp | cut -d' ' -f1)
+        COCOA_LIB=${PMC_LIB:-cocoa_amd/libcocoa_hip.so} timeout -s KILL 120 rocprofv3 --pmc $grp -d $O/spmc_${n}_$TAG -o run --output-format csv -- $SHORT \
+          > $O/spmc_${n}_$TAG.log 2>&1 || exit $?
+      done
+      python3 tools/pmc_kernels.py $O $TAG ;;
     gramprof)
       COCOA_LIB=build/diag/libcocoa_hip.so timeout -k 10 200 python3 tools/prof_gram.py cocoa+ \
         > $O/prof_gram_$TAG.json 2> $O/prof_gram_$TAG.err || exit $? ;;
+    ab)
+      for v in ${VARIANTS:-base}; do
+        lib=cocoa_amd/libcocoa_hip.so; [ "$v" = base ] || lib=build/v_$v/libcocoa_hip.so
+        COCOA_LIB=$lib timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-gap ${BENCH_ARGS} \
+          > $O/ab_${v}_$TAG.json 2> $O/ab_${v}_$TAG.err || exit $?
+        python3 -c "import json;d=json.loads(open('$O/ab_${v}_$TAG.json').readlines()[-1]);k=d['kernel_ms'];print('$v', 'step', round(d['ms_per_step'],4), 'solver', round(k['solver'],4), 'gram', round(k['gram'],4), 'eval', round(k['eval'],4), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

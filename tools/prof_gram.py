@@ -31,16 +31,20 @@ def main():
     nwg = e.K_loc * ((sh.H + 15) // 16)
     gram_phases = dict(zip(["meta_zero", "load_hot_image", "-", "hot_product", "store", "cold_insert", "cold_probe", "-"],
                            (allp[e.K_loc * 32:e.K_loc * 32 + 8] / nwg).tolist()))
-    raw = full[:, :16].reshape(e.K_loc, 4, 4)
-    mem = full[:, 16:20].mean(axis=0)
-    roles = ["chain", "memory", "loader", "fetch0"]
+    # solver_gram.h: [k][32] = waves 0..5 at 4 w (wait cycles, total cycles), memory
+    # wave c's phase cycles at 24 + 4 c
+    raw = full[:, :24].reshape(e.K_loc, 6, 4)
+    roles = ["chain", "fetch0", "memory0", "memory1", "loader", "fetch1"]
+    nb = (sh.H + 15) // 16
     out = {"method": method, "kernel_ms": {k: v["total_ms"] / max(v["launches"], 1) for k, v in st.items()},
            "waves": {r: {"wait_cyc_mean": float(raw[:, i, 0].mean()), "total_cyc_mean": float(raw[:, i, 1].mean()),
                          "wait_frac": float(raw[:, i, 0].sum() / max(raw[:, i, 1].sum(), 1))}
                      for i, r in enumerate(roles)},
            "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
-           "memory_phases_cyc_per_batch": dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
-                                                   (mem / ((sh.H + 15) // 16)).tolist())),
+           "memory_phases_cyc_per_batch": {
+               "memory%d" % c: dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
+                                        (full[:, 24 + 4 * c:28 + 4 * c].mean(axis=0) / nb).tolist()))
+               for c in (0, 1)},
            "gram_phase_cyc_per_wg": gram_phases}
     print(json.dumps(out))
 
