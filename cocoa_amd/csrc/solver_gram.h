@@ -8,7 +8,7 @@
 //
 //   x_s . deltaW_s = base_s + sum_{j in window, j < s} c_j * G(s, j)
 //
-//   base_s  = x_s . deltaW as of a batch boundary four batches back, gathered
+//   base_s  = x_s . deltaW as of a batch boundary kGNB = 3 batches back, gathered
 //             off the chain by a helper wave;
 //   G(s, j) = x_s . x_j, the Gram entries of nearby steps, computed before the
 //             round by gram_kernel (the sampled rows are known in advance:
@@ -17,7 +17,7 @@
 //             coefficient of step j (CoCoA.scala:181).
 //
 // The chain wave keeps one accumulator per lane: lane l holds the pending
-// correction of the step in window slot l (slot = step mod 64, four batches
+// correction of the step in window slot l (slot = step mod 48, three batches
 // of 16).  Step j reads its own accumulator (v_readlane), applies the update
 // rule, and adds c_j * G(., j) to every pending lane -- one FMA, no memory
 // access and no reduction on the dependent path.
@@ -27,7 +27,7 @@
 //   memory x2  -- one per column class (device column parity): per batch b,
 //                 deltaW += c_j x_j for the steps of batch b on the class's
 //                 columns (fp64 atomics into the partition's private slice),
-//                 then the gathers of x_s . deltaW for batch b+4 on them,
+//                 then the gathers of x_s . deltaW for batch b+3 on them,
 //                 software-pipelined one batch deep (issued now, summed next
 //                 time) into the class's partial base;
 //   loader     -- per-step records (constants of the update rule, the next
@@ -39,12 +39,14 @@
 // helper that is merely busy with a later batch.
 //
 // Ordering of the deltaW slice: base(b) must contain exactly the updates of
-// batches <= b-4.  A column belongs to one class, so one memory wave issues,
-// in this order, the atomics of batch b-4 to it and then the gathers of
+// batches <= b-3.  A column belongs to one class, so one memory wave issues,
+// in this order, the atomics of batch b-3 to it and then the gathers of
 // base(b), and the atomics of batch b-3 only after those gathers: one wave,
-// one address stream, so the gathers see batch b-4 and nothing later.
+// one address stream, so the gathers see batch b-3 and nothing later.
 // Batches b-3 .. b reach the steps of batch b through the Gram corrections
-// (window of 64 steps = 4 batches of 16).
+// (window of 48 steps = 3 batches of 16; lanes 48..63 of the chain idle.  A
+// 64-step window measured the same solver time with 18% more Gram-row work,
+// a 32-step one a 1.5% slower solver: r03 A/B).
 //
 // Numerics: fast mode (fused multiply-adds, reassociated dots, atomics); the
 // results agree with the strict path / oracle within the north_star
@@ -76,7 +78,7 @@ namespace cocoa {
 constexpr int kGB = 16;                  // steps per batch
 constexpr int kGSlots = 64;              // lanes; Gram-row stride (doubles)
 #ifndef COCOA_GWIN
-#define COCOA_GWIN 64
+#define COCOA_GWIN 48
 #endif
 constexpr int kGW = COCOA_GWIN;          // window slots (steps): slot of step s = s mod kGW
 constexpr int kGNB = kGW / kGB;          // batches in the window
@@ -129,14 +131,14 @@ __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F
 
 // ================================================================ Gram ==
 // Gt[k][j][slot] = x_s . x_j for the step s of window slot `slot` in j's
-// window [16 floor(j/16), +64) with s > j; 0 otherwise.
-// One workgroup per (partition, batch of 16 updaters); its 64 partners are the
+// window [16 floor(j/16), +kGW) with s > j; 0 otherwise.
+// One workgroup per (partition, batch of 16 updaters); its kGW partners are the
 // steps of the window (the updaters are partners 0..15).  The window's
 // entries are packed partner by partner and loaded at once (256 per unit, up
 // to kGramNU units in registers, owners found branch-free): one round trip to
 // memory instead of one per row.  Then
 //   hot columns (device index < kGHot, the most frequent): a dense image
-//     XP[p][c] of the 64 partners; G_hot = XP[0..15] XP^T with lanes =
+//     XP[p][c] of the partners; G_hot = XP[0..15] XP^T with lanes =
 //     partners and the updater values broadcast from LDS;
 //   cold columns: an LDS hash (column -> list of (updater, value)) of the
 //     updaters' cold entries, filled tile by tile (kGramTile packed positions
@@ -150,8 +152,8 @@ constexpr int kGramCH = kGramNU * kGramThreads;
 constexpr int kGHotS = kGHot + 1;    // XP row stride (doubles)
 
 struct GramLds {
-    double XP[kGSlots][kGHotS];      // hot image of the partners (updaters = rows 0..15)
-    double acc[kGB][kGSlots];        // G of the updaters against the window
+    double XP[kGW][kGHotS];          // hot image of the partners (updaters = rows 0..15)
+    double acc[kGB][kGW];            // G of the updaters against the window
     int32_t tkey[kGramTable];
     int32_t thead[kGramTable];
     double eval[kGramTile];
@@ -213,8 +215,8 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
         L.pcum[lane + 1] = inc;
         if (lane == 0) L.pcum[0] = 0;
     }
-    for (int i = tid; i < kGSlots * kGHotS; i += kGramThreads) (&L.XP[0][0])[i] = 0.0;
-    for (int i = tid; i < kGB * kGSlots; i += kGramThreads) (&L.acc[0][0])[i] = 0.0;
+    for (int i = tid; i < kGW * kGHotS; i += kGramThreads) (&L.XP[0][0])[i] = 0.0;
+    for (int i = tid; i < kGB * kGW; i += kGramThreads) (&L.acc[0][0])[i] = 0.0;
     __syncthreads();
     phase(0);
     const int32_t T = L.pcum[P], Q16 = L.pcum[U];
@@ -361,14 +363,17 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
     {
         double h0 = 0.0, h1 = 0.0;
         const int u0 = 2 * wv;
+        const int pl = min(lane, kGW - 1);  // lanes past the window: discarded
 #pragma unroll 8
         for (int c = 0; c < kGHot; ++c) {
-            const double xp = L.XP[lane][c];
+            const double xp = L.XP[pl][c];
             h0 = fma(L.XP[u0][c], xp, h0);
             h1 = fma(L.XP[u0 + 1][c], xp, h1);
         }
-        L.acc[u0][lane] += h0;  // sole writer of (u, lane) now
-        L.acc[u0 + 1][lane] += h1;
+        if (lane < kGW) {
+            L.acc[u0][lane] += h0;  // sole writer of (u, lane) now
+            L.acc[u0 + 1][lane] += h1;
+        }
     }
     __syncthreads();
     phase(3);
@@ -377,7 +382,7 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
     double* out = a.gt + ((size_t)k * a.nbatch * kGB + j0) * kGSlots;
     const int slot = lane < kGW ? ((g % kGNB) * kGB + lane) % kGW : lane;
     for (int u = wv; u < kGB; u += kGramThreads / 64) {
-        const double v = (u < U && lane > u && lane < P) ? L.acc[u][lane] : 0.0;
+        const double v = (u < U && lane > u && lane < P) ? L.acc[u][min(lane, kGW - 1)] : 0.0;
         __builtin_nontemporal_store(v, out + (size_t)u * kGSlots + slot);
     }
     phase(4);
@@ -406,7 +411,7 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
 // first (cocoa_set_train), so a row's entries of one class are one contiguous
 // run.  Each class has its own fetch wave, LDS sub-ring and memory wave: the
 // memory wave of class c scatters and gathers only columns of class c, so the
-// per-column order "scatter of batch b, then gathers of batch b+4" still holds
+// per-column order "scatter of batch b, then gathers of batch b+3" still holds
 // inside one wave's address stream, and the two memory waves -- the issue-
 // bound part of the round -- run on different SIMDs.  The chain adds the two
 // partial bases.
@@ -495,15 +500,10 @@ __device__ __forceinline__ int gram_owner(const int32_t* excl, int32_t q) {
     return lo;
 }
 
-// 4 bytes per lane from global memory straight into LDS (lds + 4 * lane).
-// Cache policy of the streams read once per round (CSR entries of the sampled
-// rows, Gram rows): COCOA_GRAM_NT = 2 marks them nt (MI355X_MICROARCH.md
-// nt-weights), so they pass L2 without evicting the deltaW slices.
-#ifndef COCOA_GRAM_NT
-#define COCOA_GRAM_NT 0
-#endif
+// 4 bytes per lane from global memory straight into LDS (lds + 4 * lane).  (nt
+// on these once-read streams measured no different: r03 A/B, 3.03 vs 3.04 ms)
 __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, COCOA_GRAM_NT);
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
 
 // 0 for a unit of the batch (u < nu), 0xFF (row: no entry) past it.  The row byte is
@@ -538,7 +538,7 @@ __device__ __forceinline__ double gram_rule(double u, double aa) {
 // Roles (kGThreads threads, one workgroup per partition):
 //   chain        -- the H dependent steps;
 //   memory c     -- per batch b: deltaW += c_j x_j on class-c columns (batch b),
-//                   then the gathers x_s . deltaW of batch b+4 on class-c columns,
+//                   then the gathers x_s . deltaW of batch b+3 on class-c columns,
 //                   their products summed one batch later into base[c];
 //   loader       -- records (update-rule constants, alpha forwarding marks) and
 //                   the per-class row layouts, up to kGRing batches ahead;
@@ -741,72 +741,6 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     } else if (wv == kWFetch0 || wv == kWFetch1) {
         // -------------------------------------------------------- fetch --
         const int c = wv == kWFetch0 ? 0 : 1;
-#ifdef COCOA_FETCH2
-        // Per batch: the entry offsets of all its units first (owners by four
-        // interleaved binary searches), then the previous batch's DMA is drained and
-        // published, then this batch's DMA goes out: the DMA latency of batch x-1
-        // hides behind batch x's address work instead of ending every batch.  The
-        // ring-space wait for batch x comes after batch x-1 is published (the memory
-        // waves free space only after consuming it: no cycle through the wait).
-        int32_t prev = -1;
-        for (int32_t x = 0; x < NB; ++x) {
-            if (!wait_ge(&S.cnt[kCLoad], x + 1, abortf, a.status, pw)) break;
-            const GLay& L = S.lay[x % kGRing][c];
-            const int32_t pos = L.pos, nu = L.nu, T = L.T;
-            const bool staged = pos >= 0 && nu > 0;
-            int64_t ee[kGMaxU];
-            uint32_t ro[kGMaxU];
-            if (staged) {
-#pragma unroll
-                for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
-                    if (u0 < nu) {
-                        int o[4];
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) o[t] = 0;
-#pragma unroll
-                        for (int st = kGB / 2; st >= 1; st >>= 1) {
-#pragma unroll
-                            for (int t = 0; t < 4; ++t)
-                                if (L.sx[o[t] + st] <= (u0 + t) * 64 + lane) o[t] += st;
-                        }
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const int32_t q = (u0 + t) * 64 + lane;
-                            ee[u0 + t] = L.sb[o[t]] + (q - L.sx[o[t]]);
-                            ro[u0 + t] = (q < T) ? (uint32_t)o[t] : 0xFFu;
-                        }
-                    }
-                }
-            }
-            if (prev >= 0) {
-                vm_drain();  // batch prev's DMA writes are in LDS
-                wave_lds_sync();
-                if (lane == 0) lds_release(&S.cnt[kCFetch + c], prev + 1);
-            }
-            if (staged && !wait_ge(&S.cnt[kCFreed + c], pos + nu * 64 - kGSub * 64, abortf, a.status, pw)) break;
-            if (staged) {
-#pragma unroll
-                for (int u = 0; u < kGMaxU; ++u) {
-                    if (u < nu) {
-                        uint8_t* ub = S.ring[ring_unit(c, pos, u)];
-                        if (ro[u] != 0xFFu) {
-                            const int64_t e = ee[u];
-                            lds_dma4(a.col + e, ub + kGOCol);
-                            lds_dma4((const uint32_t*)(a.val + e), ub + kGOLo);
-                            lds_dma4((const uint32_t*)(a.val + e) + 1, ub + kGOHi);
-                        }
-                        ub[kGORow + lane] = (uint8_t)ro[u];
-                    }
-                }
-            }
-            prev = x;
-        }
-        if (prev >= 0) {
-            vm_drain();
-            wave_lds_sync();
-            if (lane == 0) lds_release(&S.cnt[kCFetch + c], prev + 1);
-        }
-#else
         for (int32_t x = 0; x < NB; ++x) {
             if (!wait_ge(&S.cnt[kCLoad], x + 1, abortf, a.status, pw)) break;
             const GLay& L = S.lay[x % kGRing][c];
@@ -831,7 +765,6 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCFetch + c], x + 1);
         }
-#endif
     } else if (wv == kWMem0 || wv == kWMem1) {
         // ------------------------------------------------------- memory --
         const int c = wv == kWMem0 ? 0 : 1;  // this wave's column class
@@ -859,7 +792,6 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         for (int32_t b = 0; b < NB; ++b) {
             if (!wait_ge(&S.cnt[kCChain], b + 1, abortf, a.status, pw)) break;  // the chain finished batch b
             if (a.prof) tph = __builtin_readcyclecounter();
-#ifdef COCOA_MEM2
             // Scatter of batch b first, its LDS reads before the drain: the ring entries
             // and coefficients of b are read into registers while the gathers of batch
             // b+3 are still in flight; the drain then only orders those gathers before
@@ -948,89 +880,6 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 xin = -1;
             }
             stamp(1);
-#else
-            // every load of the previous iteration has landed (step 1 needs the gathers
-            // anyway): the compiler then knows no register is still being written and
-            // issues step 3's loads back to back instead of waiting before each one
-            vm_drain();
-            // 1. products of the gathers in flight -> this class's part of the base of
-            //    batch xin.  Each unit's product goes to (its row, lane mod 32) with a
-            //    fire-and-forget LDS add (lanes l and l + 32 share a slot: different
-            //    LDS lane groups, no conflict); 4 lanes per row add the slots up.
-            if (xin >= 0) {
-                if (lane < kGPart) {
-#pragma unroll
-                    for (int i = 0; i < kGB; ++i) part[i][lane] = 0.0;
-                }
-                wave_lds_sync();
-#pragma unroll
-                for (int u = 0; u < kGMaxU; ++u) {
-                    if (u < xnu) {
-                        const int row = min((int)((hrow[u / 6] >> (5 * (u % 6))) & 31u), kGB);  // 31: no entry
-                        __hip_atomic_fetch_add(&part[row][lane & (kGPart - 1)], hv[u] * dw[u], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-                wave_lds_sync();
-                const int rr = lane >> 2, qq = (lane & 3) * (kGPart / 4);
-                double s4 = 0.0;
-#pragma unroll
-                for (int t = 0; t < kGPart / 4; ++t) s4 += part[rr][qq + t];
-                s4 += dpp_row_d<0xB1>(s4);  // quad_perm [1,0,3,2]
-                s4 += dpp_row_d<0x4E>(s4);  // quad_perm [2,3,0,1]
-                if ((lane & 3) == 0) S.base[c][(xin % kGNB) * kGB + rr] = s4;
-                wave_lds_sync();
-                if (lane == 0) lds_release(&S.cnt[kCBase + c], xin + 1);
-                xin = -1;
-            }
-            stamp(0);
-            // 2. deltaW += c_j x_j on this class's columns for the steps of batch b
-            //    (CoCoA.scala:181-185)
-            {
-                const GLay& L = S.lay[b % kGRing][c];
-                const double* cf = S.coef + (b % kGRing) * (2 * kGB);
-                const int32_t pos = L.pos, nu = L.nu;
-                if (pos >= 0) {
-                    if (!fetched(b)) break;
-                    // groups of 8 units: the LDS reads of a group go out together (reading
-                    // past the batch is harmless: those lanes get row 0xFF)
-                    // (every read of a group before its first atomic: an LDS atomic may
-                    // alias them in the compiler's view and would serialise the group)
-                    for (int32_t u0 = 0; u0 < nu; u0 += 8) {
-                        int rw[8];
-                        int32_t cl[8];
-                        double vl[8], cc[8];
-#pragma unroll
-                        for (int t = 0; t < 8; ++t) {
-                            uint32_t r8;
-                            ring_get(S, ring_unit(c, pos, u0 + t), lane, cl[t], vl[t], r8);
-                            rw[t] = r8 | gram_pad(u0 + t, nu);
-                        }
-#pragma unroll
-                        for (int t = 0; t < 8; ++t) cc[t] = cf[rw[t] & (2 * kGB - 1)];  // row 0xFF: a zero slot
-                        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                        for (int t = 0; t < 8; ++t)
-                            if (cc[t] != 0.0 && !(COCOA_DIAG_ON && (a.diag & 1))) dw_add(cl[t], vl[t] * cc[t]);
-                    }
-                } else {
-                    // a batch too long to stage: straight from the CSR, row by row
-                    for (int i = 0; i < kGB; ++i) {
-                        const double cv = cf[i];
-                        if (cv == 0.0) continue;
-                        const int32_t z = L.sx[i + 1] - L.sx[i];
-                        const int64_t rb = L.sb[i];
-                        for (int32_t e = lane; e < z; e += 64) dw_add(a.col[rb + e], a.val[rb + e] * cv);
-                    }
-                }
-                wave_lds_sync();
-                if (lane == 0) {
-                    lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
-                    if (pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
-                }
-            }
-            stamp(1);
-#endif
             // 3. gathers of batch x = b + kGNB on this class's columns: they see batch
             //    b's updates (issued above, same wave, same addresses) and nothing later
             //    (the next atomics go out after step 1 has consumed these loads)
@@ -1107,7 +956,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             for (int i = 0; i < 4; ++i) a.prof[(size_t)k * 32 + 24 + 4 * c + i] = ph[i];
     } else if (wv == kWChain) {
         // -------------------------------------------------------- chain --
-        // lane = window slot (step mod 64): sdot = base + Gram corrections
+        // lane = window slot (step mod kGW): sdot = base + Gram corrections
         const int32_t ahead = MODE != MODE_MBCD ? kGGt + 2 : 0;  // kCLoad needed for batch g: g + 1 + kGNB (records), g + 6 (Gram rows)
         bool ok = wait_ge(&S.cnt[kCLoad], MODE != MODE_MBCD ? ahead : min(kGNB + 1, NB), abortf, a.status, pw);
         double acc = 0.0;
@@ -1119,8 +968,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             if (PROJ) R.AA = aa;
         }
         wave_lds_sync();
-        // One batch.  Alpha of batch g+4 is loaded at the start of batch g (rows met
-        // again in batches g .. g+4 are forwarded instead) and written into its
+        // One batch.  Alpha of batch g+3 is loaded at the start of batch g (rows met
+        // again in batches g .. g+3 are forwarded instead) and written into its
         // records at the end of batch g+1, a batch after the load: `aissue` / `afill`
         // alternate between two registers (no copy of a register still being loaded).
         auto batch = [&](int32_t g, double& aissue, const double& afill) -> bool {
@@ -1193,7 +1042,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     acc = fma(cf, gcur[i], acc);
                 }
                 if (fwm & (1u << i)) {
-                    // a later step (<= 79 steps on) samples the same row: its aa is nt
+                    // a later step (< kGWin steps on) samples the same row: its aa is nt
                     const double nts = readlane_d(nt, slot0 + i);
                     const int32_t sf = __builtin_amdgcn_readlane(rF, slot0 + i);
                     const int32_t sp = g * kGB + ((sf - g * kGB) & (2 * kGSlots - 1));
@@ -1227,10 +1076,10 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             }
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCChain], g + 1);
-            // this quarter now accumulates for batch g+4
+            // this batch's lanes now accumulate for batch g+kGNB
             if (mine) acc = 0.0;
-            // alpha of batch g+3 (loaded at the start of batch g-1 by the previous
-            // quarter), unless a forward already set it
+            // alpha of batch g+kGNB-1 (loaded at the start of batch g-1 by the lanes
+            // of batch g-1), unless a forward already set it
             const int32_t g3 = g + kGNB - 1;
             if (MODE != MODE_LSGD && g >= 1 && g3 < NB && lane / kGB == (g + kGNB - 1) % kGNB) {
                 GRec& R3 = S.rec[(g3 % kGRing) * kGB + (lane & (kGB - 1))];
