@@ -165,7 +165,7 @@ struct cocoa_ctx {
     int32_t K_loc = 0, K_glob = 0, part_begin = 0, d = 0;
     Csr tr;
     DevBuf sqn, rowflags, part_ptr;
-    DevBuf row_z0;  // fast mode: entries of column class 0 per row (they lead the row), see set_train_impl
+    DevBuf row_zc;  // fast mode: per row, ends of the column-class runs (4 int32), see set_train_impl
     std::vector<int64_t> h_part_ptr;
     bool any_dup = false;
     bool tr_dense = false;  // every row stores columns 0..d-1 in order (val = X[n][d])
@@ -237,7 +237,7 @@ struct cocoa_ctx {
         if (gstream) HIPCHK(hipStreamSynchronize(gstream));
         pre_t = -1;
     }
-    DevBuf plan_beg, plan_z, plan_z0, plan_y, plan_q, plan_xw;
+    DevBuf plan_beg, plan_z, plan_zc, plan_y, plan_q, plan_xw;
     // x.w of every train row for the current w, written by the fast eval pass
     // (eval v4) and reused by the next round's plan; false once w moves
     DevBuf row_xw;
@@ -710,17 +710,17 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
         pcol.resize((size_t)std::max<int64_t>(nnz, 1));
         for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];
     }
-    // Fast mode: every row stores the entries of column class 0 (even device
-    // column) before those of class 1, each class in stored order, so that the
-    // Gram solver's two memory waves (solver_gram.h) each stream one contiguous
-    // run per row.  Only the fast kernels see this order (their dots are
+    // Fast mode: every row stores its entries class by class (class of device
+    // column c = c % kGramClasses), each class in stored order, so that each of
+    // the Gram solver's memory waves (solver_gram.h) streams one contiguous run
+    // per row.  Only the fast kernels see this order (their dots are
     // reassociated anyway); strict mode keeps the stored order of every row.
     std::vector<double> pval;
-    std::vector<int32_t> z0v;
+    std::vector<int32_t> zcv;
     const bool split_classes = !ctx->strict && !dense_in && !ctx->tr_dense && nnz > 0;  // dense rows: val is X[n][d]
     if (split_classes) {
         pval.resize((size_t)nnz);
-        z0v.resize((size_t)std::max<int64_t>(n_rows, 1));
+        zcv.resize((size_t)std::max<int64_t>(n_rows, 1) * 4);
         std::vector<int32_t> ncol((size_t)std::max<int64_t>(nnz, 1));
         const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         std::vector<std::thread> th;
@@ -728,15 +728,20 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
             th.emplace_back([&, tix] {
                 for (int64_t r = n_rows * tix / T; r < n_rows * (tix + 1) / T; ++r) {
                     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
-                    int64_t c0 = 0;
-                    for (int64_t q = b; q < e; ++q) c0 += (pcol[(size_t)q] & 1) == 0;
-                    int64_t i0 = b, i1 = b + c0;
+                    int64_t cnt[kGramClasses] = {}, at[kGramClasses];
+                    for (int64_t q = b; q < e; ++q) ++cnt[pcol[(size_t)q] % kGramClasses];
+                    int64_t run = b;
+                    for (int c = 0; c < kGramClasses; ++c) {
+                        at[c] = run;
+                        run += cnt[c];
+                    }
+                    for (int c = 0; c < 4; ++c)  // ends of the class runs (row-relative); unused: z
+                        zcv[(size_t)r * 4 + c] = (int32_t)((c < kGramClasses - 1 ? at[c] + cnt[c] : e) - b);
                     for (int64_t q = b; q < e; ++q) {
-                        const int64_t dst = (pcol[(size_t)q] & 1) == 0 ? i0++ : i1++;
+                        const int64_t dst = at[pcol[(size_t)q] % kGramClasses]++;
                         ncol[(size_t)dst] = pcol[(size_t)q];
                         pval[(size_t)dst] = val[q];
                     }
-                    z0v[(size_t)r] = (int32_t)c0;
                 }
             });
         for (auto& t : th) t.join();
@@ -756,9 +761,9 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
     }
     upload_padded(ctx->tr.val, split_classes ? pval.data() : val, sizeof(double) * (size_t)nnz, s);
     if (split_classes)
-        upload(ctx->row_z0, z0v.data(), sizeof(int32_t) * (size_t)n_rows, s);
+        upload(ctx->row_zc, zcv.data(), sizeof(int32_t) * 4 * (size_t)n_rows, s);
     else
-        ctx->row_z0.free();
+        ctx->row_zc.free();
     upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
@@ -1080,10 +1085,10 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         const size_t steps = (size_t)std::max<int64_t>((int64_t)K * H, 1);
         ctx->plan_beg.alloc(steps * sizeof(int64_t));
         ctx->plan_z.alloc(steps * sizeof(int32_t));
-        if (ctx->row_z0.p)
-            ctx->plan_z0.alloc(steps * sizeof(int32_t));
+        if (ctx->row_zc.p)
+            ctx->plan_zc.alloc(steps * 4 * sizeof(int32_t));
         else
-            ctx->plan_z0.free();
+            ctx->plan_zc.free();
         ctx->plan_y.alloc(steps * sizeof(double));
         ctx->plan_q.alloc(steps * sizeof(double));
         ctx->plan_xw.alloc(steps * sizeof(double));
@@ -1095,7 +1100,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     } else {
         ctx->plan_beg.free();
         ctx->plan_z.free();
-        ctx->plan_z0.free();
+        ctx->plan_zc.free();
         ctx->plan_y.free();
         ctx->plan_q.free();
         ctx->plan_xw.free();
@@ -1126,7 +1131,7 @@ static GramArgs gram_args(cocoa_ctx* c, const int32_t* samples, double* gt) {
     ga.H = c->P.local_iters;
     ga.nbatch = c->nbatch;
     ga.gt = gt;
-    ga.prof = c->sa.prof ? c->sa.prof + (size_t)c->K_loc * 32 : nullptr;  // phase sums of this launch
+    ga.prof = c->sa.prof ? c->sa.prof + (size_t)c->K_loc * kProfStride : nullptr;  // phase sums of this launch
     return ga;
 }
 
@@ -1206,8 +1211,8 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             // the Gram solver splits x.w_local = x.w + x.deltaW
             pa.need_xw = !c->use_dense && (c->method != COCOA_METHOD_COCOA || c->use_gram);
             pa.xw_cache = (c->xw_cached && !c->strict) ? c->row_xw.as<double>() : nullptr;
-            pa.row_z0 = c->plan_z0.p ? c->row_z0.as<int32_t>() : nullptr;
-            pa.z0 = c->plan_z0.p ? c->plan_z0.as<int32_t>() : nullptr;
+            pa.row_zc = c->plan_zc.p ? c->row_zc.as<int32_t>() : nullptr;
+            pa.zc = c->plan_zc.p ? c->plan_zc.as<int32_t>() : nullptr;
             pa.beg = c->plan_beg.as<int64_t>();
             pa.z = c->plan_z.as<int32_t>();
             pa.py = c->plan_y.as<double>();
@@ -1244,7 +1249,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.samples = smp;
             g.plan_beg = c->plan_beg.as<int64_t>();
             g.plan_z = c->plan_z.as<int32_t>();
-            g.plan_z0 = c->plan_z0.p ? c->plan_z0.as<int32_t>() : nullptr;
+            g.plan_zc = c->plan_zc.p ? c->plan_zc.as<int32_t>() : nullptr;
             g.plan_y = c->plan_y.as<double>();
             g.plan_q = c->plan_q.as<double>();
             g.plan_xw = c->plan_xw.as<double>();
@@ -2427,7 +2432,7 @@ extern "C" int cocoa_solver_profile(cocoa_ctx* ctx, int enable) {
     GROUP_REJECT(ctx, "cocoa_solver_profile");
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     if (enable) {
-        ctx->prof.alloc_zero(sizeof(uint64_t) * ((size_t)ctx->K_loc * 32 + 8), ctx->stream);  // + gram_kernel phases
+        ctx->prof.alloc_zero(sizeof(uint64_t) * ((size_t)ctx->K_loc * kProfStride + 8), ctx->stream);  // + gram_kernel phases
         ctx->sa.prof = ctx->prof.as<uint64_t>();
     } else {
         ctx->sa.prof = nullptr;
@@ -2439,7 +2444,7 @@ extern "C" int cocoa_solver_profile_read(cocoa_ctx* ctx, uint64_t* out, int64_t 
     CAPI_BEGIN(ctx)
     GROUP_REJECT(ctx, "cocoa_solver_profile_read");
     require(out && ctx->prof.p, COCOA_E_STATE, "solver profiling not enabled");
-    const size_t n = std::min<size_t>((size_t)count, (size_t)ctx->K_loc * 32 + 8);
+    const size_t n = std::min<size_t>((size_t)count, (size_t)ctx->K_loc * kProfStride + 8);
     HIPCHK(hipMemcpyAsync(out, ctx->prof.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     CAPI_END(ctx)

@@ -14,6 +14,16 @@ namespace cocoa {
 enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2, MODE_LSGD = 3 };
 
 constexpr int kWave = 64;
+// deltaW column classes of the Gram solver (solver_gram.h): device column c is
+// in class c % kGramClasses, each with its own memory and fetch wave.  In fast
+// mode every row stores its entries class by class (cocoa_set_train), with the
+// run ends of classes 0 .. kGramClasses-2 per row in row_zc (4 int32 a row).
+#ifndef COCOA_GNC
+#define COCOA_GNC 2
+#endif
+constexpr int kGramClasses = COCOA_GNC;
+static_assert(kGramClasses == 2 || kGramClasses == 4, "column classes");
+constexpr int kProfStride = 64;     // solver profile words per partition (diagnostics)
 constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
 #ifndef COCOA_REG_CHUNKS
 #define COCOA_REG_CHUNKS 4
@@ -96,10 +106,10 @@ struct PlanArgs {
     int32_t H;
     int32_t need_xw;
     const double* xw_cache;   // per-row x.w of the current w from the last fast eval, or null
-    const int32_t* row_z0;    // per row: entries of column class 0 (fast mode), or null
+    const int32_t* row_zc;    // per row: 4 int32, ends of the class runs 0 .. kGramClasses-2 (fast mode), or null
     int64_t* beg;
     int32_t* z;
-    int32_t* z0;              // per step: row_z0 of its row (when row_z0)
+    int32_t* zc;              // per step: row_zc of its row, 4 int32 (when row_zc)
     double* py;
     double* pq;
     double* xw;
@@ -123,7 +133,7 @@ struct GramSolverArgs {
     const int32_t* samples;
     const int64_t* plan_beg;
     const int32_t* plan_z;
-    const int32_t* plan_z0;   // per step: entries of column class 0 (they lead the row), or null: all
+    const int32_t* plan_zc;   // per step: 4 int32, ends of the rows' class runs (row_zc), or null: all class 0
     const double* plan_y;
     const double* plan_q;
     const double* plan_xw;

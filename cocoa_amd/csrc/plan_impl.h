@@ -48,7 +48,10 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         __builtin_nontemporal_store(a.y[gr], a.py + g);
         __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
         __builtin_nontemporal_store(xw, a.xw + g);
-        if (a.row_z0) __builtin_nontemporal_store(a.row_z0[gr], a.z0 + g);
+        if (a.row_zc) {
+            typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(*(const i32x4*)(a.row_zc + 4 * gr), (i32x4*)(a.zc + 4 * g));
+        }
     }
 }
 

@@ -379,11 +379,11 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
     phase(3);
     // Gt rows of the block's updaters: slot of partner p = (j0 + p) mod kGW (slots
     // past the window: zero)
-    double* out = a.gt + ((size_t)k * a.nbatch * kGB + j0) * kGSlots;
-    const int slot = lane < kGW ? ((g % kGNB) * kGB + lane) % kGW : lane;
+    double* out = a.gt + ((size_t)k * a.nbatch * kGB + j0) * kGW;
+    const int slot = ((g % kGNB) * kGB + lane) % kGW;
     for (int u = wv; u < kGB; u += kGramThreads / 64) {
         const double v = (u < U && lane > u && lane < P) ? L.acc[u][min(lane, kGW - 1)] : 0.0;
-        __builtin_nontemporal_store(v, out + (size_t)u * kGSlots + slot);
+        if (lane < kGW) __builtin_nontemporal_store(v, out + (size_t)u * kGW + slot);
     }
     phase(4);
 }
@@ -406,28 +406,38 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
 // so u is huge for any aa.  MbCD (MinibatchCD.scala:104): A = 0, so B = 0.
 //
 // Column classes.  deltaW's columns are split into kGNC classes (device
-// column parity: the device order is by frequency, so the classes carry
-// about the same entries); in fast mode every row stores its class-0 entries
-// first (cocoa_set_train), so a row's entries of one class are one contiguous
-// run.  Each class has its own fetch wave, LDS sub-ring and memory wave: the
-// memory wave of class c scatters and gathers only columns of class c, so the
-// per-column order "scatter of batch b, then gathers of batch b+3" still holds
-// inside one wave's address stream, and the two memory waves -- the issue-
-// bound part of the round -- run on different SIMDs.  The chain adds the two
+// column c in class c % kGNC: the device order is by frequency, so the classes
+// carry about the same entries); in fast mode every row stores its entries
+// class by class (cocoa_set_train), so a row's entries of one class are one
+// contiguous run.  Each class has its own fetch wave, LDS sub-ring and memory
+// wave: the memory wave of class c scatters and gathers only columns of class
+// c, so the per-column order "scatter of batch b, then gathers of batch b+3"
+// still holds inside one wave's address stream, and the memory waves -- the
+// issue-bound part of the round -- run side by side.  The chain adds the
 // partial bases.
 constexpr int kGWin = kGW + kGB;         // loader's look-back for alpha forwarding: the window + 1 batch
-constexpr int kGNC = 2;                  // column classes = memory waves = fetch waves
+constexpr int kGNC = kGramClasses;       // column classes = memory waves = fetch waves
 constexpr int kGE = 8192;                // staged entries (LDS ring positions), all classes
 constexpr int kGSub = kGE / 64 / kGNC;   // 64-entry units of one class's sub-ring
 constexpr int kGUnitB = 64 * 13;         // bytes of one 64-entry ring unit
 constexpr int kGOCol = 0, kGOLo = 256, kGOHi = 512, kGORow = 768;  // its fields
 constexpr int kGMaxU = kGSub / 4;        // units of one class of a staged batch (4 live batches per
                                          // sub-ring); larger batches go direct
-constexpr int kGThreads = 64 * (2 + 2 * kGNC);
 constexpr int kGGt = 4;                  // Gram-row ring (batches)
-constexpr int kGPart = 32;               // product slots per row (lanes l and l + 32 share one)
-// wave roles (waves w and w + 4 share a SIMD: the memory waves get one each)
-constexpr int kWChain = 0, kWFetch0 = 1, kWMem0 = 2, kWMem1 = 3, kWLoader = 4, kWFetch1 = 5;
+constexpr int kGPart = kGNC == 2 ? 32 : 16;  // product slots per row (lanes l, l + kGPart, ... share one)
+// Wave roles.  Wave w of the workgroup runs on SIMD w % 4, and which waves
+// share a SIMD matters (r03 A/B on C2, two classes): chain + loader on one
+// SIMD and the two fetch waves on another, 2.97 ms; chain + fetch 0 and
+// loader + fetch 1, 2.85 ms; the memory waves keep a SIMD each.  Four classes
+// (ten waves, a memory wave beside the chain) measured 3.35 ms.
+enum GRole : int { kRChain = 0, kRLoader = 1, kRMem = 2, kRFetch = 2 + kGNC, kRIdle = 2 + 2 * kGNC };
+#ifndef COCOA_GLAYOUT
+#define COCOA_GLAYOUT kRChain, kRLoader, kRMem, kRMem + 1, kRFetch, kRFetch + 1
+#endif
+constexpr int kGRoles[] = {COCOA_GLAYOUT};
+constexpr int kGWaves = (int)(sizeof(kGRoles) / sizeof(int));
+constexpr int kGThreads = 64 * kGWaves;
+static_assert(kGNC == 2 || kGWaves == 2 + 2 * kGNC, "wave layout");
 
 struct GRec {                          // one step (64 B)
     double B, Y, AE, YA;               // AE, YA: set by the chain (its alpha prefetch or a forward)
@@ -451,10 +461,10 @@ struct GLay {                          // one batch's rows of one class, for the
 // counters (LDS, release / acquire); kCScat .. kCFetch: one per class
 constexpr int kCChain = 0, kCLoad = 1, kCAbort = 2, kCScat = 3, kCBase = kCScat + kGNC, kCFreed = kCBase + kGNC,
               kCFetch = kCFreed + kGNC;
-static_assert(kCFetch + kGNC <= 16, "counters");
+static_assert(kCFetch + kGNC <= 32, "counters");
 
 struct GramSolverLds {
-    int cnt[16];
+    int cnt[32];
     double lsgd_s;                     // MODE_LSGD: s after the last step (loader -> epilogue)
     int32_t lsgd_keep, lsgd_pad;       //   and whether wInit survived (no zero shrink)
     GRec rec[kGRing * kGB];            // ring: (b % kGRing) * kGB + i
@@ -462,7 +472,7 @@ struct GramSolverLds {
     GLay lay[kGRing][kGNC];            // same ring (loader -> fetch / memory waves)
     double base[kGNC][kGSlots];        // partial base_s per class and slot (memory waves -> chain)
     double part[kGNC][kGB + 1][kGPart];  // memory wave: row partial sums of a batch's products (+ a sink row)
-    double gring[kGGt][kGB][kGSlots];  // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
+    double gring[kGGt][kGB][kGW];      // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
     int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
     // staged entries (fetch waves -> memory waves), 64 per ring unit: columns, value
     // low words, value high words (the LDS DMA moves 4 bytes a lane), row bytes
@@ -554,13 +564,18 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int k = blockIdx.x;
     const int32_t H = a.H, NB = (H + kGB - 1) / kGB;
+    int role = kRIdle;
+#pragma unroll
+    for (int i = 0; i < kGWaves; ++i)
+        if (wv == i) role = kGRoles[i];
+    role = __builtin_amdgcn_readfirstlane(role);
     const int64_t p0 = a.part_ptr[k];
     const int32_t nl = (int32_t)(a.part_ptr[k + 1] - p0);
     const size_t g0 = (size_t)k * H;
     double* dwk = a.dw + (size_t)k * a.d;
     // working alpha of the partition (global), plus a sink at [nl] for the padding steps
     double* alv = a.alpha_work + p0 + k;
-    const double* gt = a.gt + (size_t)k * a.nbatch * kGB * kGSlots;
+    const double* gt = a.gt + (size_t)k * a.nbatch * kGB * kGW;
     int* abortf = &S.cnt[kCAbort];
 
     if (MODE != MODE_LSGD) {
@@ -570,7 +585,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     for (int i = tid; i < kGNC * kGSlots; i += kGThreads) (&S.base[0][0])[i] = 0.0;  // batches 0 .. kGNB-1
     for (int32_t i = tid; i < hot; i += kGThreads) hotl[i] = 0.0;
     for (int i = tid; i < kGRing * 2 * kGB; i += kGThreads) S.coef[i] = 0.0;  // zero slots: rows past a batch
-    if (tid < 16) S.cnt[tid] = 0;
+    if (tid < 32) S.cnt[tid] = 0;
     __syncthreads();
     if (tid < kGNC) S.cnt[kCBase + tid] = kGNB;
     __syncthreads();
@@ -578,7 +593,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     uint64_t* pw = a.prof ? &wait_cycles : nullptr;
     const uint64_t t_start = a.prof ? __builtin_readcyclecounter() : 0;
 
-    if (wv == kWLoader) {
+    if (role == kRLoader) {
         // ------------------------------------------------------- loader --
         int32_t cursor[kGNC];  // sub-ring position of the next staged batch, per class
 #pragma unroll
@@ -586,7 +601,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         for (int i = lane; i < 2 * kGSlots; i += 64) S.smpwin[i] = -2;
         // the step's inputs one batch ahead (registers)
         const int i = lane & (kGB - 1);
-        int32_t xr = nl, xz = 0, xz0 = 0;
+        int32_t xr = nl, xz = 0;
+        int32_t xzc[kGNC - 1];  // ends of the class runs 0 .. kGNC-2 in the row
         double xy = 0.0, xq = 0.0, xxw = 0.0;
         int64_t xbeg = 0;
         double ls = 1.0;   // MODE_LSGD: s before the batch (SGD.scala:119-120), wave-uniform
@@ -594,7 +610,9 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         auto load = [&](int32_t b) {
             const int32_t j = b * kGB + i;
             xr = nl;
-            xz = xz0 = 0;
+            xz = 0;
+#pragma unroll
+            for (int c = 0; c < kGNC - 1; ++c) xzc[c] = 0;
             xy = xq = xxw = 0.0;
             xbeg = 0;
             if (lane < kGB && j < H) {
@@ -604,7 +622,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 xxw = a.plan_xw[g0 + j];
                 xbeg = a.plan_beg[g0 + j];
                 xz = a.plan_z[g0 + j];
-                xz0 = a.plan_z0 ? a.plan_z0[g0 + j] : xz;
+#pragma unroll
+                for (int c = 0; c < kGNC - 1; ++c) xzc[c] = a.plan_zc ? a.plan_zc[4 * (g0 + j) + c] : xz;
             }
         };
         load(0);
@@ -625,17 +644,22 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             if (b < NB) {
                 const int32_t j = b * kGB + i;
                 const bool valid = lane < kGB && j < H;
-                const int32_t r = xr, z = xz, z0 = xz0;
+                const int32_t r = xr, z = xz;
+                int32_t ze[kGNC + 1];  // class c: entries [beg + ze[c], beg + ze[c+1])
+                ze[0] = 0;
+#pragma unroll
+                for (int c = 0; c < kGNC - 1; ++c) ze[c + 1] = xzc[c];
+                ze[kGNC] = z;
                 const double y = xy, q = xq, xw = xxw;
                 const int64_t beg = xbeg;
                 if (b + 1 < NB) load(b + 1);
                 const int32_t w0 = b * kGB - kGW;  // look-back window: steps [w0, w0 + kGWin)
                 if (MODE != MODE_LSGD && lane < kGB) S.smpwin[j & (2 * kGSlots - 1)] = valid ? r : -2;
-                // the rows' runs of each class: class 0 = entries [beg, beg + z0), class 1 = the rest
+                // the rows' runs of each class
                 int32_t inc[kGNC], T[kGNC], nu[kGNC];
 #pragma unroll
                 for (int c = 0; c < kGNC; ++c) {
-                    const int32_t zc = c == 0 ? z0 : z - z0;
+                    const int32_t zc = ze[c + 1] - ze[c];
                     inc[c] = wave_incl_scan(lane < kGB ? zc : 0);
                     T[c] = __shfl(inc[c], kGB - 1, 64);
                     nu[c] = (T[c] + 63) >> 6;
@@ -707,7 +731,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     GLay& L = S.lay[b % kGRing][c];
                     if (lane < kGB) {
                         L.sx[lane + 1] = inc[c];
-                        L.sb[lane] = c == 0 ? beg : beg + z0;
+                        L.sb[lane] = beg + ze[c];
                     }
                     if (lane == 0) {
                         L.sx[0] = 0;
@@ -726,10 +750,11 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             }
             const int32_t xg = b - kGGt;  // Gram rows of batch xg: 16 rows x 64 slots
             if (MODE != MODE_MBCD && xg >= 0 && xg < NB) {
-                const uint32_t* src = (const uint32_t*)(gt + (size_t)xg * kGB * kGSlots);
+                const uint32_t* src = (const uint32_t*)(gt + (size_t)xg * kGB * kGW);
                 uint32_t* dst = (uint32_t*)&S.gring[xg % kGGt][0][0];
+                static_assert((2 * kGB * kGW) % 64 == 0, "Gram-row DMA");
 #pragma unroll 8
-                for (int t = 0; t < 2 * kGB * kGSlots / 64; ++t) lds_dma4(src + t * 64 + lane, dst + t * 64);
+                for (int t = 0; t < 2 * kGB * kGW / 64; ++t) lds_dma4(src + t * 64 + lane, dst + t * 64);
             }
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCLoad], b + 1);
@@ -738,9 +763,9 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             S.lsgd_s = ls;
             S.lsgd_keep = lkeep;
         }
-    } else if (wv == kWFetch0 || wv == kWFetch1) {
+    } else if (role >= kRFetch && role < kRIdle) {
         // -------------------------------------------------------- fetch --
-        const int c = wv == kWFetch0 ? 0 : 1;
+        const int c = role - kRFetch;
         for (int32_t x = 0; x < NB; ++x) {
             if (!wait_ge(&S.cnt[kCLoad], x + 1, abortf, a.status, pw)) break;
             const GLay& L = S.lay[x % kGRing][c];
@@ -765,9 +790,9 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCFetch + c], x + 1);
         }
-    } else if (wv == kWMem0 || wv == kWMem1) {
+    } else if (role >= kRMem && role < kRFetch) {
         // ------------------------------------------------------- memory --
-        const int c = wv == kWMem0 ? 0 : 1;  // this wave's column class
+        const int c = role - kRMem;  // this wave's column class
         const bool bases = MODE != MODE_MBCD;
         double hv[kGMaxU], dw[kGMaxU];  // in-flight gathers: staged value (x hot deltaW), loaded deltaW (or 1)
         uint32_t hrow[(kGMaxU + 5) / 6];  //   and their rows (5 bits per unit, 31 = no entry)
@@ -953,8 +978,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         }
         vm_drain();  // the last atomics land before the kernel ends
         if (a.prof && lane == 0)
-            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * 32 + 24 + 4 * c + i] = ph[i];
-    } else if (wv == kWChain) {
+            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * kProfStride + 48 + 4 * c + i] = ph[i];
+    } else if (role == kRChain) {
         // -------------------------------------------------------- chain --
         // lane = window slot (step mod kGW): sdot = base + Gram corrections
         const int32_t ahead = MODE != MODE_MBCD ? kGGt + 2 : 0;  // kCLoad needed for batch g: g + 1 + kGNB (records), g + 6 (Gram rows)
@@ -999,8 +1024,9 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 acc += bsum;
             }
             double gcur[kGB];
+            const int gl = min(lane, kGW - 1);  // lanes past the window: any value (never read back)
 #pragma unroll
-            for (int i = 0; i < kGB; ++i) gcur[i] = MODE != MODE_MBCD ? S.gring[g % kGGt][i][lane] : 0.0;
+            for (int i = 0; i < kGB; ++i) gcur[i] = MODE != MODE_MBCD ? S.gring[g % kGGt][i][gl] : 0.0;
             double* cfo = S.coef + (g % kGRing) * (2 * kGB);
             const int slot0 = q4 * kGB;
             // this batch's records in the lanes of its quarter (lane slot0 + i holds step
@@ -1099,7 +1125,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         }
     }
     if (a.prof && lane == 0) {
-        uint64_t* pr = a.prof + (size_t)k * 32 + wv * 4;  // [k][32]: waves 0..5 at 0..23, memory phases at 24..31
+        uint64_t* pr = a.prof + (size_t)k * kProfStride + wv * 4;  // [k][64]: waves at 4 wv, memory phases at 48 + 4 c
         pr[0] = wait_cycles;
         pr[1] = __builtin_readcyclecounter() - t_start;
     }

@@ -26,15 +26,16 @@ def main():
         e.round(t)
     e.sync()
     st = e.kernel_stats()
-    allp = e.solver_profile_read(e.K_loc * 32 + 8).astype(np.float64)
-    full = allp[:e.K_loc * 32].reshape(e.K_loc, 32)
+    S = 64  # kProfStride (kernels.h)
+    allp = e.solver_profile_read(e.K_loc * S + 8).astype(np.float64)
+    full = allp[:e.K_loc * S].reshape(e.K_loc, S)
     nwg = e.K_loc * ((sh.H + 15) // 16)
     gram_phases = dict(zip(["meta_zero", "load_hot_image", "-", "hot_product", "store", "cold_insert", "cold_probe", "-"],
-                           (allp[e.K_loc * 32:e.K_loc * 32 + 8] / nwg).tolist()))
-    # solver_gram.h: [k][32] = waves 0..5 at 4 w (wait cycles, total cycles), memory
-    # wave c's phase cycles at 24 + 4 c
+                           (allp[e.K_loc * S:e.K_loc * S + 8] / nwg).tolist()))
+    # solver_gram.h: [k][64] = wave w at 4 w (wait cycles, total cycles), memory
+    # wave c's phase cycles at 48 + 4 c; roles in the default layout (COCOA_GLAYOUT)
     raw = full[:, :24].reshape(e.K_loc, 6, 4)
-    roles = ["chain", "fetch0", "memory0", "memory1", "loader", "fetch1"]
+    roles = ["chain", "loader", "memory0", "memory1", "fetch0", "fetch1"]
     nb = (sh.H + 15) // 16
     out = {"method": method, "kernel_ms": {k: v["total_ms"] / max(v["launches"], 1) for k, v in st.items()},
            "waves": {r: {"wait_cyc_mean": float(raw[:, i, 0].mean()), "total_cyc_mean": float(raw[:, i, 1].mean()),
@@ -43,7 +44,7 @@ def main():
            "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
            "memory_phases_cyc_per_batch": {
                "memory%d" % c: dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
-                                        (full[:, 24 + 4 * c:28 + 4 * c].mean(axis=0) / nb).tolist()))
+                                        (full[:, 48 + 4 * c:52 + 4 * c].mean(axis=0) / nb).tolist()))
                for c in (0, 1)},
            "gram_phase_cyc_per_wg": gram_phases}
     print(json.dumps(out))
