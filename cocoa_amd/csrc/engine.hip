@@ -185,6 +185,8 @@ struct cocoa_ctx {
     // row tiles of the fast evaluation pass (kEvalTile entries)
     DevBuf tiles, t_tiles;
     int64_t n_tiles = 0, n_t_tiles = 0;
+    DevBuf dtiles, t_dtiles;  // eval_dma_kernel's tiles (kEvalDmaEntries / kEvalDmaRows)
+    int64_t n_dtiles = 0, n_t_dtiles = 0;
     // device feature order (see cocoa_set_train)
     std::vector<int32_t> perm, inv;
     std::vector<int64_t> n_hot_nnz;
@@ -237,6 +239,14 @@ struct cocoa_ctx {
         if (gstream) HIPCHK(hipStreamSynchronize(gstream));
         pre_t = -1;
     }
+    // pipelined evaluation (cocoa_eval_async): the objectives of a snapshot of
+    // (w, alpha) on estream, beside the next round; results in h_eval[4..7]
+    hipStream_t estream = nullptr;
+    hipEvent_t e_round = nullptr, e_done = nullptr;
+    bool eval_pending = false;  // snapshots taken (cocoa_eval_async), result not yet collected
+    bool eval_fired = false;    //   and its kernels enqueued on estream
+    DevBuf w_snap, alpha_snap, eval_part2, eval_out2;
+    void eval_quiesce();        // the pending evaluation (if any) runs to completion and is dropped
     DevBuf plan_beg, plan_z, plan_zc, plan_y, plan_q, plan_xw;
     // x.w of every train row for the current w, written by the fast eval pass
     // (eval v4) and reused by the next round's plan; false once w moves
@@ -313,6 +323,12 @@ struct cocoa_ctx {
             (void)hipStreamDestroy(gstream);
             (void)hipEventDestroy(g_ready);
             for (auto e : s_done) (void)hipEventDestroy(e);
+        }
+        if (estream) {
+            (void)hipStreamSynchronize(estream);
+            (void)hipStreamDestroy(estream);
+            (void)hipEventDestroy(e_round);
+            (void)hipEventDestroy(e_done);
         }
         delete comm;
         if (zstream) {
@@ -461,7 +477,9 @@ static void upload_padded(DevBuf& b, const void* src, size_t bytes, hipStream_t 
 
 // Row tiles for the fast eval pass: whole rows, <= kEvalTile entries and rows
 // per tile; a row longer than kEvalTile is a tile of its own.
-static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStream_t s, int64_t cap = kEvalTile) {
+static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStream_t s, int64_t cap = kEvalTile,
+                          int64_t row_cap = -1) {
+    if (row_cap < 0) row_cap = cap;
     std::vector<int64_t> t{0};
     int64_t r = 0;
     while (r < n) {
@@ -469,7 +487,7 @@ static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStr
         if (row_ptr[r + 1] - e0 > cap) {
             ++r;
         } else {
-            while (r < n && row_ptr[r + 1] - e0 <= cap && r - start < cap) ++r;
+            while (r < n && row_ptr[r + 1] - e0 <= cap && r - start < row_cap) ++r;
         }
         t.push_back(r);
     }
@@ -633,6 +651,7 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
                            int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
     const bool dense_in = col == nullptr;
     ctx->gram_quiesce();  // a Gram prefetch reads the CSR being replaced
+    ctx->eval_quiesce();  // so does a pending evaluation
     require(num_parts >= 1 && part_ptr && row_ptr && y && n_rows >= 0 && num_features >= 1, COCOA_E_ARG,
             "cocoa_set_train: bad argument");
     require(part_begin >= 0 && num_parts_global >= part_begin + num_parts, COCOA_E_ARG,
@@ -769,6 +788,7 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s, eval_tile_entries());
+    ctx->n_dtiles = make_tiles(row_ptr, n_rows, ctx->dtiles, s, kEvalDmaEntries, kEvalDmaRows);
     if (dense_in) {
         ctx->compact_ready = false;  // dense rows touch every column: no compact slices
         ctx->col_local.free();
@@ -799,6 +819,7 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
 static void set_test_impl(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t* col, const double* val,
                           const double* y, int64_t n_rows) {
     const bool dense_in = col == nullptr;
+    ctx->eval_quiesce();  // a pending evaluation reads the test rows being replaced
     require(ctx->d > 0, COCOA_E_STATE, "cocoa_set_test: call cocoa_set_train first");
     require(row_ptr && y && n_rows >= 0, COCOA_E_ARG, "cocoa_set_test: bad argument");
     if (!dense_in) check_csr(row_ptr, col, n_rows, ctx->d);
@@ -822,6 +843,7 @@ static void set_test_impl(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t*
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s, eval_tile_entries());
+    ctx->n_t_dtiles = make_tiles(row_ptr, n_rows, ctx->t_dtiles, s, kEvalDmaEntries, kEvalDmaRows);
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     if (ctx->inited) {
@@ -944,6 +966,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     ctx->alpha_work.alloc(sizeof(double) * (size_t)(std::max<int64_t>(n, 1) + K));  // + a sink per partition
     if (ctx->zstream) HIPCHK(hipStreamSynchronize(ctx->zstream));  // no re-zeroing in flight
     ctx->gram_quiesce();                                            // no Gram prefetch in flight
+    ctx->eval_quiesce();                                            // nor a pending evaluation
     ctx->zpending[0] = ctx->zpending[1] = false;
     ctx->zero_owed = -1;
     // the fast Gram solver on data with a compact layout: slices of max_u
@@ -1140,6 +1163,7 @@ static GramArgs gram_args(cocoa_ctx* c, const int32_t* samples, double* gt) {
 // which recv_init (a multi-device context's peer copy) or the communicator's
 // chain_recv puts into dw_sum first.
 typedef void (*recv_fn)(cocoa_ctx* c, void* user);
+static void eval_fire(cocoa_ctx* ctx);
 static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* chain_init = nullptr,
                       recv_fn recv_init = nullptr, void* recv_user = nullptr) {
     require(c->inited, COCOA_E_STATE, "cocoa_round: call cocoa_init first");
@@ -1327,6 +1351,9 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         c->timed(COCOA_K_APPLY, [&] { launch_scale(c->w.as<double>(), d, 1.0 - (step * c->P.lambda), s); });
         c->mult = step * c->scaling;
     }
+    // a pipelined evaluation of the previous state (cocoa_eval_async) goes out
+    // now, behind this round's solver launch
+    eval_fire(c);
     if (chain_init) {  // the fold of ranks < rank (rank > 0)
         if (recv_init)
             recv_init(c, recv_user);
@@ -1534,20 +1561,27 @@ static void finish(const cocoa_ctx* c, double hinge, double alpha_sum, double w2
 
 // The evaluation pass of one (sub-)context, enqueued: the rank-local sums land
 // in h_eval (pinned) once the stream reaches them.
-static void eval_launch(cocoa_ctx* ctx) {
+// async (cocoa_eval_async): on estream, from the (w, alpha) snapshots, into
+// eval_part2 / eval_out2 and h_eval[4..7]; no row x.w kept (the next round's
+// plan forms x.w itself)
+static void eval_launch(cocoa_ctx* ctx, bool async = false) {
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    require(async || !ctx->eval_pending, COCOA_E_STATE,
+            "an evaluation is pending: collect it with cocoa_eval_wait first");
+    hipStream_t st = async ? ctx->estream : ctx->stream;
     const bool dense_eval = !ctx->strict && ctx->tr_dense && (!ctx->has_test || ctx->te_dense || ctx->te.n == 0) &&
                             dense_eval_fits(ctx->d);
-    if (!dense_eval) {  // the CSR passes read the column arrays
+    if (!dense_eval) {  // the CSR passes read the column arrays (on the context's stream)
         ensure_cols(ctx->tr, ctx->d, ctx->stream);
         if (ctx->has_test) ensure_cols(ctx->te, ctx->d, ctx->stream);
     }
+    if (async) HIPCHK(hipStreamWaitEvent(ctx->estream, ctx->e_round, 0));  // the snapshots are taken
     EvalArgs e{};
     e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     e.col = ctx->tr.col.as<int32_t>();
     e.val = ctx->tr.val.as<double>();
     e.y = ctx->tr.y.as<double>();
-    e.alpha = ctx->alpha.as<double>();
+    e.alpha = async ? ctx->alpha_snap.as<double>() : ctx->alpha.as<double>();
     e.n = ctx->tr.n;
     e.t_row_ptr = ctx->has_test ? ctx->te.row_ptr.as<int64_t>() : nullptr;
     e.t_col = ctx->has_test ? ctx->te.col.as<int32_t>() : nullptr;
@@ -1556,31 +1590,42 @@ static void eval_launch(cocoa_ctx* ctx) {
     e.t_val = ctx->has_test ? ctx->te.val.as<double>() : nullptr;
     e.t_y = ctx->has_test ? ctx->te.y.as<double>() : nullptr;
     e.n_test = ctx->has_test ? ctx->te.n : 0;
-    e.w = ctx->w.as<double>();
+    e.w = async ? ctx->w_snap.as<double>() : ctx->w.as<double>();
     e.d = ctx->d;
     e.part_ptr = ctx->part_ptr.as<int64_t>();
     e.perm = ctx->d_perm.as<int32_t>();
     e.K = ctx->K_loc;
-    e.partials = ctx->eval_part.as<double>();
-    e.out = ctx->eval_out.as<double>();
+    e.partials = async ? ctx->eval_part2.as<double>() : ctx->eval_part.as<double>();
+    e.out = async ? ctx->eval_out2.as<double>() : ctx->eval_out.as<double>();
     e.row_scratch = ctx->row_scratch.as<double>();
     e.tiles = ctx->tiles.as<int64_t>();
     e.n_tiles = ctx->n_tiles;
     e.t_tiles = ctx->has_test ? ctx->t_tiles.as<int64_t>() : nullptr;
     e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles : 0;
-    ctx->timed(COCOA_K_EVAL, [&] {
+    e.dtiles = ctx->dtiles.as<int64_t>();
+    e.n_dtiles = ctx->n_dtiles;
+    e.t_dtiles = ctx->has_test ? ctx->t_dtiles.as<int64_t>() : nullptr;
+    e.n_t_dtiles = ctx->has_test ? ctx->n_t_dtiles : 0;
+    e.nnz = ctx->tr.nnz;
+    e.t_nnz = ctx->has_test ? ctx->te.nnz : 0;
+    ctx->timed_on(st, COCOA_K_EVAL, [&] {
         if (ctx->strict)
-            launch_eval_strict(e, ctx->stream);
+            launch_eval_strict(e, st);
         else {
-            e.row_xw = ctx->row_xw.as<double>();
+            e.row_xw = async ? nullptr : ctx->row_xw.as<double>();
             if (dense_eval)
-                launch_eval_dense(e, ctx->stream);  // rows read as X[n][d]: 8 B per entry
+                launch_eval_dense(e, st);  // rows read as X[n][d]: 8 B per entry
             else
-                launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), ctx->stream);
-            ctx->xw_cached = true;  // the next round's plan reuses these x.w (stream order)
+                launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), st);
+            ctx->xw_cached = !async;  // the next round's plan reuses these x.w (stream order)
         }
     });
-    HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (async) {
+        HIPCHK(hipMemcpyAsync(ctx->h_eval + 4, ctx->eval_out2.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(ctx->e_done, st));
+    } else {
+        HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+    }
 }
 
 struct EvalLocal {
@@ -1652,6 +1697,67 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
         cm.allreduce(counts, 2, false, ctx->stream);  // integers: exact in any order
     }
     finish(ctx, hinge, alpha_sum, w2, (int64_t)counts[0], (int64_t)counts[1], out);
+    CAPI_END(ctx)
+}
+
+// Pipelined evaluation: one device, one rank, fast mode (the strict and
+// multi-rank merges need the exchange in order; those contexts use cocoa_eval).
+extern "C" int cocoa_eval_async(cocoa_ctx* ctx) {
+    CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_eval_async");
+    require(!ctx->strict && !(ctx->comm && ctx->comm->world > 1), COCOA_E_STATE,
+            "cocoa_eval_async: fast mode on a single rank only (use cocoa_eval)");
+    require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    require(!ctx->eval_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_wait first");
+    if (!ctx->estream) {
+        HIPCHK(hipStreamCreateWithFlags(&ctx->estream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ctx->e_round, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ctx->e_done, hipEventDisableTiming));
+    }
+    const size_t nw = sizeof(double) * (size_t)ctx->d, na = sizeof(double) * (size_t)std::max<int64_t>(ctx->tr.n, 1);
+    if (ctx->w_snap.bytes < nw) ctx->w_snap.alloc(nw);
+    if (ctx->alpha_snap.bytes < na) ctx->alpha_snap.alloc(na);
+    const size_t np = sizeof(double) * (size_t)std::max<int64_t>(4 * 2048, 2 * ctx->K_loc + 8);
+    if (ctx->eval_part2.bytes < np) ctx->eval_part2.alloc(np);
+    if (ctx->eval_out2.bytes < 8 * sizeof(double)) ctx->eval_out2.alloc(8 * sizeof(double));
+    // snapshots on the context's stream (the next round moves w and alpha); the
+    // evaluation itself is enqueued by the next round right after its solver
+    // launch (eval_fire), so the solver's workgroups hold their CUs first and the
+    // evaluation fills the idle ones beside the Gram rows.  (Enqueued at once, it
+    // raced the next round's plan and solver for CUs: 3.30 -> 3.74 ms per C2 step.)
+    HIPCHK(hipMemcpyAsync(ctx->w_snap.p, ctx->w.p, nw, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->alpha_snap.p, ctx->alpha.p, na, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->e_round, ctx->stream));
+    ctx->eval_pending = true;
+    ctx->eval_fired = false;
+    ctx->xw_cached = false;  // the next round's plan forms x.w itself
+    CAPI_END(ctx)
+}
+
+static void eval_fire(cocoa_ctx* ctx) {
+    if (!ctx->eval_pending || ctx->eval_fired) return;
+    eval_launch(ctx, true);
+    ctx->eval_fired = true;
+}
+
+void cocoa_ctx::eval_quiesce() {
+    if (!eval_pending) return;
+    eval_fire(this);
+    HIPCHK(hipEventSynchronize(e_done));
+    eval_pending = false;
+}
+
+extern "C" int cocoa_eval_wait(cocoa_ctx* ctx, cocoa_eval_result* out) {
+    CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_eval_wait");
+    require(out != nullptr, COCOA_E_ARG, "null out");
+    require(ctx->eval_pending, COCOA_E_STATE, "cocoa_eval_wait: no evaluation pending (cocoa_eval_async)");
+    eval_fire(ctx);  // no round was issued after cocoa_eval_async
+    HIPCHK(hipEventSynchronize(ctx->e_done));
+    ctx->eval_pending = false;
+    check_status(ctx);
+    const double* h = ctx->h_eval + 4;
+    finish(ctx, h[0], h[1], h[2], (int64_t)h[3], (int64_t)(ctx->has_test ? ctx->te.n : 0), out);
     CAPI_END(ctx)
 }
 

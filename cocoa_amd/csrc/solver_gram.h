@@ -424,7 +424,10 @@ constexpr int kGOCol = 0, kGOLo = 256, kGOHi = 512, kGORow = 768;  // its fields
 constexpr int kGMaxU = kGSub / 4;        // units of one class of a staged batch (4 live batches per
                                          // sub-ring); larger batches go direct
 constexpr int kGGt = 4;                  // Gram-row ring (batches)
-constexpr int kGPart = kGNC == 2 ? 32 : 16;  // product slots per row (lanes l, l + kGPart, ... share one)
+#ifndef COCOA_GPART
+#define COCOA_GPART (kGNC == 2 ? 32 : 16)
+#endif
+constexpr int kGPart = COCOA_GPART;      // product slots per row (lanes l, l + kGPart, ... share one)
 // Wave roles.  Wave w of the workgroup runs on SIMD w % 4, and which waves
 // share a SIMD matters (r03 A/B on C2, two classes): chain + loader on one
 // SIMD and the two fetch waves on another, 2.97 ms; chain + fetch 0 and
@@ -853,7 +856,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     }
                 }
                 stamp(3);
-                vm_drain();  // the gathers of batch b+3 have read the slice
+                if (bases) vm_drain();  // the gathers of batch b+kGNB-1 have read the slice (MbCD: no gathers)
                 stamp(0);
                 if (pos >= 0) {
 #pragma unroll

@@ -182,6 +182,16 @@ class Engine:
         C.check(C.lib().cocoa_eval(self.h, ctypes.byref(r)), self.h)
         return r.as_dict()
 
+    def eval_async(self):
+        """cocoa_eval_async: enqueue the objectives of the current state beside
+        the next round (one device, fast mode); collect them with eval_wait."""
+        C.check(C.lib().cocoa_eval_async(self.h), self.h)
+
+    def eval_wait(self):
+        r = C.EvalResult()
+        C.check(C.lib().cocoa_eval_wait(self.h, ctypes.byref(r)), self.h)
+        return r.as_dict()
+
     def eval_finish(self, hinge_sum, alpha_sum, w_sq, err, test_rows):
         r = C.EvalResult()
         C.check(C.lib().cocoa_eval_finish(self.h, hinge_sum, alpha_sum, w_sq, int(err), int(test_rows),

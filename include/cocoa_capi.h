@@ -212,6 +212,16 @@ int cocoa_round(cocoa_ctx *ctx, int32_t t);
  * fields are the reference's values; with several, all-reduce hinge_sum,
  * alpha_sum and test_err_count and finish with cocoa_eval_finish. */
 int cocoa_eval(cocoa_ctx *ctx, cocoa_eval_result *out);
+/* The same evaluation, pipelined (one device, one rank, fast mode): enqueue
+ * the objectives of the current (w, alpha) -- snapshots taken on the context's
+ * stream -- on a side stream and return at once, so the next cocoa_round runs
+ * beside it; cocoa_eval_wait returns exactly what cocoa_eval would have
+ * returned for that state.  The reference prints these after round t before
+ * starting round t+1 (CoCoA.scala:51-56); here the host learns them while
+ * round t+1 is already on the GPU.  One evaluation may be pending at a time;
+ * cocoa_eval refuses while one is. */
+int cocoa_eval_async(cocoa_ctx *ctx);
+int cocoa_eval_wait(cocoa_ctx *ctx, cocoa_eval_result *out);
 int cocoa_eval_finish(const cocoa_ctx *ctx, double hinge_sum, double alpha_sum, double w_sqnorm,
                       int64_t test_err_count, int64_t test_rows, cocoa_eval_result *out);
 

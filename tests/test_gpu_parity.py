@@ -537,3 +537,58 @@ def test_dense_rows_double_stream(method, strict):
         wr = run.w()
         assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
         assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
+
+
+# ------------------------------------------------------ pipelined evaluation --
+@pytest.mark.parametrize("method", ["cocoa+", "localsgd"])
+def test_eval_async_equals_eval_and_overlaps_next_round(c1, method):
+    """cocoa_eval_async snapshots (w, alpha) and evaluates beside the next round:
+    what eval_wait returns is bitwise what cocoa_eval returns for that state
+    (same kernels, same fixed-order reductions), and a pipelined run's
+    trajectory matches the in-line one within the fast-mode tolerance (the
+    Gram solver's atomics differ from run to run)."""
+    tr, te = c1
+    H = 150
+    a = engine(tr, te, strict=False)
+    b = engine(tr, te, strict=False)
+    for e in (a, b):
+        e.init(method, tr.n, 10, H, 1e-3)
+    inline, piped = [], []
+    for t in range(1, 7):
+        a.round(t)
+        inline.append(a.eval())
+        b.round(t)
+        if t > 1:
+            piped.append(b.eval_wait())  # round t-1's, collected while round t runs
+        b.eval_async()
+    piped.append(b.eval_wait())
+    for t, (x, y) in enumerate(zip(inline, piped), 1):
+        assert abs(x["primal"] - y["primal"]) <= REL * abs(x["primal"]), t
+        if method == "cocoa+":
+            assert abs(x["gap"] - y["gap"]) <= REL * abs(x["primal"]), t
+        assert x["test_err_count"] == y["test_err_count"], t
+    # bitwise on one state
+    b.eval_async()
+    z = b.eval_wait()
+    w = b.eval()
+    assert z["primal"].hex() == w["primal"].hex() and z["dual"].hex() == w["dual"].hex()
+    assert z["test_err_count"] == w["test_err_count"]
+
+
+def test_eval_async_state_errors(c1):
+    tr, te = c1
+    e = engine(tr, te, strict=False)
+    e.init("cocoa+", tr.n, 4, 50, 1e-3)
+    e.round(1)
+    with pytest.raises(cocoa_amd.CocoaError):
+        e.eval_wait()  # nothing pending
+    e.eval_async()
+    with pytest.raises(cocoa_amd.CocoaError):
+        e.eval_async()  # one at a time
+    with pytest.raises(cocoa_amd.CocoaError):
+        e.eval()  # in-line refused while one is pending
+    e.eval_wait()
+    s = engine(tr, te, strict=True)
+    s.init("cocoa+", tr.n, 4, 50, 1e-3)
+    with pytest.raises(cocoa_amd.CocoaError):
+        s.eval_async()  # strict: in line only

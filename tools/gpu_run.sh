@@ -77,8 +77,12 @@ for step in "$@"; do
         > $O/prof_gram_$TAG.json 2> $O/prof_gram_$TAG.err || exit $? ;;
     ab)
       for v in ${VARIANTS:-base}; do
-        lib=cocoa_amd/libcocoa_hip.so; [ "$v" = base ] || lib=build/v_$v/libcocoa_hip.so
-        COCOA_LIB=$lib timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-gap ${BENCH_ARGS} \
+        # NAME or NAME+ENVVAR=VALUE (an env setting for that run, e.g. diag+COCOA_GRAM_HOTLDS=1)
+        name=${v%%+*}; envset=""; [ "$name" = "$v" ] || envset=${v#*+}
+        lib=cocoa_amd/libcocoa_hip.so; [ "$name" = base ] || lib=build/v_$name/libcocoa_hip.so
+        [ "$name" = diag ] && lib=build/diag/libcocoa_hip.so
+        v=${v//=/_}
+        env $envset COCOA_LIB=$lib timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-gap ${BENCH_ARGS} \
           > $O/ab_${v}_$TAG.json 2> $O/ab_${v}_$TAG.err || exit $?
         python3 -c "import json;d=json.loads(open('$O/ab_${v}_$TAG.json').readlines()[-1]);k=d['kernel_ms'];print('$v', 'step', round(d['ms_per_step'],4), 'solver', round(k['solver'],4), 'gram', round(k['gram'],4), 'eval', round(k['eval'],4), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
       done ;;
