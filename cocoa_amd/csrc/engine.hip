@@ -185,8 +185,6 @@ struct cocoa_ctx {
     // row tiles of the fast evaluation pass (kEvalTile entries)
     DevBuf tiles, t_tiles;
     int64_t n_tiles = 0, n_t_tiles = 0;
-    DevBuf dtiles, t_dtiles;  // eval_dma_kernel's tiles (kEvalDmaEntries / kEvalDmaRows)
-    int64_t n_dtiles = 0, n_t_dtiles = 0;
     // device feature order (see cocoa_set_train)
     std::vector<int32_t> perm, inv;
     std::vector<int64_t> n_hot_nnz;
@@ -788,7 +786,6 @@ static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* par
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s, eval_tile_entries());
-    ctx->n_dtiles = make_tiles(row_ptr, n_rows, ctx->dtiles, s, kEvalDmaEntries, kEvalDmaRows);
     if (dense_in) {
         ctx->compact_ready = false;  // dense rows touch every column: no compact slices
         ctx->col_local.free();
@@ -843,7 +840,6 @@ static void set_test_impl(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t*
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s, eval_tile_entries());
-    ctx->n_t_dtiles = make_tiles(row_ptr, n_rows, ctx->t_dtiles, s, kEvalDmaEntries, kEvalDmaRows);
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     if (ctx->inited) {
@@ -1602,12 +1598,6 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false) {
     e.n_tiles = ctx->n_tiles;
     e.t_tiles = ctx->has_test ? ctx->t_tiles.as<int64_t>() : nullptr;
     e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles : 0;
-    e.dtiles = ctx->dtiles.as<int64_t>();
-    e.n_dtiles = ctx->n_dtiles;
-    e.t_dtiles = ctx->has_test ? ctx->t_dtiles.as<int64_t>() : nullptr;
-    e.n_t_dtiles = ctx->has_test ? ctx->n_t_dtiles : 0;
-    e.nnz = ctx->tr.nnz;
-    e.t_nnz = ctx->has_test ? ctx->te.nnz : 0;
     ctx->timed_on(st, COCOA_K_EVAL, [&] {
         if (ctx->strict)
             launch_eval_strict(e, st);

@@ -215,22 +215,12 @@ struct EvalArgs {
     // null; padded like col (the fast eval then streams 10 B per entry)
     const uint16_t* col16;
     const uint16_t* t_col16;
-    // the LDS-DMA eval (eval_dma_kernel): its own tiles (<= kEvalDmaEntries
-    // entries, <= kEvalDmaRows rows) and the entry counts that bound its reads
-    const int64_t* dtiles;
-    int64_t n_dtiles;
-    const int64_t* t_dtiles;
-    int64_t n_t_dtiles;
-    int64_t nnz, t_nnz;
 };
-constexpr int kEvalDmaEntries = 1022;  // staged 1,024 from the even entry below the tile's first
-constexpr int kEvalDmaRows = 31;       // the tile's row_ptr slice (32 int64) is one 256-B DMA piece
 
 // fast translation unit
 void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
                         hipStream_t s);
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
-bool eval_dma_enabled();  // the fast sparse eval runs eval_dma_kernel (its tiles are needed)
 int eval_fast_blocks(int64_t n, int64_t n_test);
 int eval_tile_entries();  // entries per fast-eval tile (make_tiles cap)
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);

@@ -326,224 +326,6 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(EvalArgs a) {
     }
 }
 
-// ------------------------------------------ wave-specialised streaming eval --
-// eval_ws_kernel: the fast sparse eval (OptUtils.scala:57-98) with the CSR
-// stream and the w gathers in different waves.  A loader wave moves whole
-// tiles (values, columns, the tile's row_ptr slice and labels) into an LDS
-// ring by LDS-DMA and keeps several tiles in flight, publishing each tile once
-// its counted vmcnt retires it; four compute waves sum rows (16 lanes a row)
-// from the ring with their own w gathers.  Each wave's vmcnt then holds one
-// kind of load only: the stream never waits behind a gather's register use and
-// a gather never waits for the stream (in one wave the in-order counter would
-// drain the stream at every gather).  Tiles hold <= kEvalDmaEntries entries and
-// <= kEvalDmaRows rows (1,024 staged from the even entry below the first); a
-// single longer row is summed by compute wave 0 from global memory.
-constexpr int kEWStages = 6;   // LDS ring (tiles)
-constexpr int kEWCompute = 4;  // compute waves
-constexpr int kEWThreads = 64 * (1 + kEWCompute);
-
-template <bool C16>
-struct EvalWsStage {
-    double val[1024];
-    uint32_t col[C16 ? 512 : 1024];  // uint16 pairs, or int32
-    int64_t rp[32];
-    double y[32];
-};
-template <bool C16>
-struct EvalWsLds {
-    EvalWsStage<C16> st[kEWStages];
-    int landed;            // tiles [0, landed) of the block are in the ring
-    int cons[kEWCompute];  // compute wave c has finished tiles [0, cons[c])
-    int pad[3];
-    double red[kEWThreads / 64];
-};
-
-typedef __attribute__((address_space(4))) const int64_t cint64;  // scalar (SMEM) loads: lgkmcnt, not vmcnt
-typedef __attribute__((address_space(3))) void lds_void_t;
-#define EW_DMA(src, dst, bytes) __builtin_amdgcn_global_load_lds((const void*)(src), (lds_void_t*)(dst), bytes, 0, 0)
-
-// s_waitcnt immediate for vmcnt(n) alone (gfx9: vmcnt bits [3:0] and [15:14])
-constexpr int ew_vmcnt(int n) { return (n & 15) | 0x70 | 0xF00 | (((n >> 4) & 3) << 14); }
-
-// Hand-off counters read and written with raw ds_read / ds_write: an LDS fence
-// (or an LDS access the compiler cannot separate from the DMA's LDS writes)
-// makes hipcc wait vmcnt(0) first, which would drain the loader's stream at
-// every tile.  A wave's LDS operations execute in order, so a counter written
-// after the wave's ds_reads of a stage (compute) or after the counted vmcnt
-// that retired a stage's DMA (loader) orders them for the reader; the "memory"
-// clobber keeps the compiler from moving other memory operations across.
-__device__ __forceinline__ uint32_t ew_lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ int ew_acquire(const int* p) {
-    int v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ew_lds_addr(p)) : "memory");
-    return v;
-}
-__device__ __forceinline__ void ew_release(int* p, int v) {
-    asm volatile("ds_write_b32 %0, %1" : : "v"(ew_lds_addr(p)), "v"(v) : "memory");
-}
-
-template <bool C16>
-__global__ __launch_bounds__(kEWThreads) void eval_ws_kernel(EvalArgs a) {
-    constexpr int P = (C16 ? 8 : 16) + 8 + 2;  // DMA pieces per tile (columns, values, row_ptr, y)
-    constexpr int AHEAD = C16 ? 4 : 3;         // tiles in flight
-    static_assert(P * (AHEAD - 1) < 64 && AHEAD < kEWStages, "vmcnt field / ring");
-    __shared__ EvalWsLds<C16> L;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int64_t ntr = a.n_dtiles, ntiles = ntr + a.n_t_dtiles;
-    const int64_t G = gridDim.x;
-    const int nk = blockIdx.x < ntiles ? (int)((ntiles - blockIdx.x + G - 1) / G) : 0;
-    if (tid == 0) L.landed = 0;
-    if (tid < kEWCompute) L.cons[tid] = 0;
-    __syncthreads();
-    // tile k of this block: side, rows [r0, r1), entries [e0, e1)
-    auto tile = [&](int k, bool& test, int64_t& r0, int64_t& r1, int64_t& e0, int64_t& e1) {
-        const int64_t t = blockIdx.x + (int64_t)k * G;
-        test = t >= ntr;
-        const int64_t tt = test ? t - ntr : t;
-        cint64* tl = (cint64*)(test ? a.t_dtiles : a.dtiles);
-        cint64* te = tl + (test ? a.n_t_dtiles : a.n_dtiles) + 1;
-        r0 = tl[tt];
-        r1 = tl[tt + 1];
-        e0 = te[tt];
-        e1 = te[tt + 1];
-    };
-    double hinge = 0.0, err = 0.0;
-    if (wv == 0) {
-        // ------------------------------------------------------- loader --
-        for (int k = 0; k < nk; ++k) {
-            // stage k % kEWStages last held tile k - kEWStages: every compute wave done with it
-            for (;;) {
-                int m = 1 << 30;
-#pragma unroll
-                for (int c = 0; c < kEWCompute; ++c) m = min(m, ew_acquire(&L.cons[c]));
-                if (m >= k - kEWStages + 1) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            bool test;
-            int64_t r0, r1, e0, e1;
-            tile(k, test, r0, r1, e0, e1);
-            EvalWsStage<C16>& S = L.st[k % kEWStages];
-            const int64_t base = e0 & ~(int64_t)1;
-            const double* vl = test ? a.t_val : a.val;
-            const int64_t nnz = test ? a.t_nnz : a.nnz;
-            const int64_t n = test ? a.n_test : a.n;
-            // the entry arrays carry 64 zero bytes of tail padding: reads clamp inside it
-            const int64_t vmax = (nnz + 6) & ~(int64_t)1;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) EW_DMA(vl + min(base + 2 * (64 * j + lane), vmax), &S.val[128 * j], 16);
-            if (C16) {
-                const uint16_t* cl = test ? a.t_col16 : a.col16;
-                const int64_t cmax = (nnz + 30) & ~(int64_t)1;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) EW_DMA(cl + min(base + 2 * (64 * j + lane), cmax), &S.col[64 * j], 4);
-            } else {
-                const int32_t* cl = test ? a.t_col : a.col;
-#pragma unroll
-                for (int j = 0; j < 16; ++j) EW_DMA(cl + min(base + 64 * j + lane, nnz + 15), &S.col[64 * j], 4);
-            }
-            const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
-            const double* yy = test ? a.t_y : a.y;
-            EW_DMA((const uint32_t*)rp + min(2 * r0 + lane, 2 * n + 1), &S.rp[0], 4);  // row_ptr[r0 .. r0+31]
-            EW_DMA((const uint32_t*)yy + min(2 * r0 + lane, 2 * n - 1), &S.y[0], 4);   // y[r0 .. r0+31]
-            // tile k - AHEAD + 1 is older than the AHEAD - 1 tiles issued after it
-            if (k >= AHEAD - 1) {
-                __builtin_amdgcn_s_waitcnt(ew_vmcnt(P * (AHEAD - 1)));
-                if (lane == 0) ew_release(&L.landed, k - AHEAD + 2);
-            }
-        }
-        __builtin_amdgcn_s_waitcnt(ew_vmcnt(0));
-        if (lane == 0) ew_release(&L.landed, nk);
-    } else {
-        // ------------------------------------------------------ compute --
-        const int c = wv - 1, sub = lane & 15, grp = lane >> 4;
-        for (int k = 0; k < nk; ++k) {
-            while (ew_acquire(&L.landed) < k + 1) __builtin_amdgcn_s_sleep(1);
-            bool test;
-            int64_t r0, r1, e0, e1;
-            tile(k, test, r0, r1, e0, e1);
-            const EvalWsStage<C16>& S = L.st[k % kEWStages];
-            const double* yy = test ? a.t_y : a.y;
-            if (e1 - e0 > kEvalDmaEntries) {
-                // one row longer than a tile: compute wave 0 from global memory
-                if (c == 0) {
-                    const double* vl = test ? a.t_val : a.val;
-                    double acc = 0.0;
-                    if (C16) {
-                        const uint16_t* cl = test ? a.t_col16 : a.col16;
-                        for (int64_t q = e0 + lane; q < e1; q += 64) acc = fma(vl[q], a.w[cl[q]], acc);
-                    } else {
-                        const int32_t* cl = test ? a.t_col : a.col;
-                        for (int64_t q = e0 + lane; q < e1; q += 64) acc = fma(vl[q], a.w[cl[q]], acc);
-                    }
-                    const double dot = wave_sum(acc);
-                    if (lane == 0) {
-                        if (!test) {
-                            hinge += jmax(1 - yy[r0] * dot, 0.0);
-                            if (a.row_xw) a.row_xw[r0] = dot;
-                        } else {
-                            err += (dot * yy[r0] > 0) ? 0.0 : 1.0;
-                        }
-                    }
-                }
-            } else {
-                const int64_t base = e0 & ~(int64_t)1;
-                const int nr = (int)(r1 - r0);
-                const uint16_t* c16 = (const uint16_t*)S.col;
-                // rows c*4 + grp, + 16, ...: 16 lanes a row, 4 entries a lane in flight
-                for (int r = c * 4 + grp; r < nr; r += 4 * kEWCompute) {
-                    const int b = (int)(S.rp[r] - base), e = (int)(S.rp[r + 1] - base);
-                    double acc = 0.0;
-                    for (int q0 = b + sub; q0 < e; q0 += 64) {
-                        int32_t cc[4];
-                        double vv[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int q = min(q0 + 16 * u, e - 1);  // past the row: its last entry, dropped
-                            cc[u] = C16 ? (int32_t)c16[q] : (int32_t)S.col[q];
-                            vv[u] = q0 + 16 * u < e ? S.val[q] : 0.0;
-                        }
-                        double ww[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) ww[u] = a.w[cc[u]];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) acc = fma(vv[u], ww[u], acc);
-                    }
-                    const double dot = row16_sum(acc);
-                    if (sub == 0) {
-                        if (!test) {
-                            hinge += jmax(1 - S.y[r] * dot, 0.0);
-                            if (a.row_xw) a.row_xw[r0 + r] = dot;
-                        } else {
-                            err += (dot * S.y[r] > 0) ? 0.0 : 1.0;
-                        }
-                    }
-                }
-            }
-            if (lane == 0) ew_release(&L.cons[c], k + 1);  // (the release waits for this wave's LDS reads)
-        }
-    }
-    __syncthreads();
-    const int64_t gt = (int64_t)blockIdx.x * kEWThreads + tid;
-    const int64_t gs = (int64_t)gridDim.x * kEWThreads;
-    double al = 0.0, w2 = 0.0;
-    if (a.alpha)
-        for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
-    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
-    const double s0 = block_sum_n<kEWThreads>(hinge, L.red);
-    const double s1 = block_sum_n<kEWThreads>(al, L.red);
-    const double s2 = block_sum_n<kEWThreads>(w2, L.red);
-    const double s3 = block_sum_n<kEWThreads>(err, L.red);
-    if (tid == 0) {
-        double* p = a.partials + (size_t)blockIdx.x * 4;
-        p[0] = s0;
-        p[1] = s1;
-        p[2] = s2;
-        p[3] = s3;
-    }
-}
-
 __global__ __launch_bounds__(256) void eval_final_kernel(const double* partials, int blocks, double* out) {
     __shared__ double red[4][4];
     const int tid = threadIdx.x;
@@ -586,18 +368,8 @@ static int eval_variant() {
     return v;
 }
 
-bool eval_dma_enabled() { return eval_variant() == 10; }
-
 void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
     const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
-    if (eval_variant() == 10) {  // wave-specialised: LDS-DMA stream + gathering compute waves, 2 blocks per CU
-        const int64_t nt = a.n_dtiles + a.n_t_dtiles;
-        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(nt, 512));
-        if (c16) eval_ws_kernel<true><<<nb, kEWThreads, 0, s>>>(a);
-        else eval_ws_kernel<false><<<nb, kEWThreads, 0, s>>>(a);
-        eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
-        return;
-    }
     if (eval_variant() == 8 || eval_variant() == 9) {  // 2,048-entry tiles, more blocks per CU
         const int64_t nt = a.n_tiles + a.n_t_tiles;
         if (eval_variant() == 8) {  // 512 threads, 4 blocks per CU

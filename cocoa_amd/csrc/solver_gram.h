@@ -84,7 +84,10 @@ constexpr int kGW = COCOA_GWIN;          // window slots (steps): slot of step s
 constexpr int kGNB = kGW / kGB;          // batches in the window
 static_assert(kGW % kGB == 0 && kGW <= kGSlots && kGNB >= 2, "window");
 constexpr int kGRing = 8;                // record / coefficient ring (batches)
-constexpr int kGHot = 32;                // dense hot columns of gram_kernel (device order: most frequent first)
+#ifndef COCOA_GHOT
+#define COCOA_GHOT 32
+#endif
+constexpr int kGHot = COCOA_GHOT;        // dense hot columns of gram_kernel (device order: most frequent first)
 
 // ----------------------------------------------------------- LDS handoff --
 // The hand-offs order LDS data only (records, coefficients, layouts, staged
@@ -425,7 +428,7 @@ constexpr int kGMaxU = kGSub / 4;        // units of one class of a staged batch
                                          // sub-ring); larger batches go direct
 constexpr int kGGt = 4;                  // Gram-row ring (batches)
 #ifndef COCOA_GPART
-#define COCOA_GPART (kGNC == 2 ? 32 : 16)
+#define COCOA_GPART 16  // (32: 1.4% slower, 544 fewer LDS-resident deltaW columns; r03 A/B)
 #endif
 constexpr int kGPart = COCOA_GPART;      // product slots per row (lanes l, l + kGPart, ... share one)
 // Wave roles.  Wave w of the workgroup runs on SIMD w % 4, and which waves
