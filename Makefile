@@ -59,7 +59,7 @@ variant:
 	    build/v_$(V)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o $(BUILD)/ingest.strict.o -lpthread -ldl
 
 # PMC calibration / latency micro-benchmarks (tools/gpu_run.sh pmc)
-ubench: tools/ubench/calib tools/ubench/lat tools/ubench/ldsdma
+ubench: tools/ubench/calib tools/ubench/lat tools/ubench/ldsdma tools/ubench/dma_layout
 tools/ubench/%: tools/ubench/%.hip
 	$(HIPCC) -O2 --offload-arch=$(ARCH) $< -o $@
 
