@@ -478,7 +478,7 @@ struct GramSolverLds {
     GLay lay[kGRing][kGNC];            // same ring (loader -> fetch / memory waves)
     double base[kGNC][kGSlots];        // partial base_s per class and slot (memory waves -> chain)
     double part[kGNC][kGB + 1][kGPart];  // memory wave: row partial sums of a batch's products (+ a sink row)
-    double gring[kGGt][kGB][kGW];      // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
+    alignas(16) double gring[kGGt][kGB][kGW];      // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
     int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
     // staged entries (fetch waves -> memory waves), 64 per ring unit: columns, value
     // low words, value high words (the LDS DMA moves 4 bytes a lane), row bytes
@@ -516,10 +516,15 @@ __device__ __forceinline__ int gram_owner(const int32_t* excl, int32_t q) {
     return lo;
 }
 
-// 4 bytes per lane from global memory straight into LDS (lds + 4 * lane).  (nt
-// on these once-read streams measured no different: r03 A/B, 3.03 vs 3.04 ms)
+// 4 or 16 bytes per lane from global memory straight into LDS (lds + size *
+// lane).  (nt on these once-read streams measured no different: r03 A/B, 3.03
+// vs 3.04 ms.)  The 12-byte form is no use for packed records: it writes lane l
+// at lds + 16 l, leaving every fourth word (tools/ubench/dma_layout.hip).
 __device__ __forceinline__ void lds_dma4(const void* g, void* lds) {
     __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+__device__ __forceinline__ void lds_dma16(const void* g, void* lds) {
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
 // 0 for a unit of the batch (u < nu), 0xFF (row: no entry) past it.  The row byte is
@@ -758,9 +763,9 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             if (MODE != MODE_MBCD && xg >= 0 && xg < NB) {
                 const uint32_t* src = (const uint32_t*)(gt + (size_t)xg * kGB * kGW);
                 uint32_t* dst = (uint32_t*)&S.gring[xg % kGGt][0][0];
-                static_assert((2 * kGB * kGW) % 64 == 0, "Gram-row DMA");
-#pragma unroll 8
-                for (int t = 0; t < 2 * kGB * kGW / 64; ++t) lds_dma4(src + t * 64 + lane, dst + t * 64);
+                static_assert((2 * kGB * kGW) % 256 == 0, "Gram-row DMA");
+#pragma unroll
+                for (int t = 0; t < 2 * kGB * kGW / 256; ++t) lds_dma16(src + t * 256 + 4 * lane, dst + t * 256);
             }
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCLoad], b + 1);
