@@ -6,7 +6,8 @@
 #include <cstdint>
 
 template <int SIZE>
-__global__ void probe(const uint32_t* src, uint32_t* out) {
+__global__ void probe(const uint32_t* src, uint32_t* out, int shift) {
+    src += shift;  // shift 2: 8-byte- but not 16-byte-aligned sources
     __shared__ uint32_t lds[1024];
     for (int i = threadIdx.x; i < 1024; i += 64) lds[i] = 0xEEEEEEEEu;
     __syncthreads();
@@ -27,17 +28,23 @@ int main() {
     hipMalloc(&out, 4096);
     hipMemcpy(src, h, sizeof(h), hipMemcpyHostToDevice);
     uint32_t o[1024];
-    probe<12><<<1, 64>>>(src, out);
+    probe<12><<<1, 64>>>(src, out, 0);
     hipMemcpy(o, out, 4096, hipMemcpyDeviceToHost);
     printf("size 12: first 24 dwords:");
     for (int i = 0; i < 24; ++i) printf(" %x", o[i]);
     int last = 0;
     for (int i = 0; i < 1024; ++i) if (o[i] != 0xEEEEEEEEu) last = i;
     printf("\nsize 12: last written dword %d (packed lane*12 -> 191; lane*16 -> 255)\n", last);
-    probe<16><<<1, 64>>>(src, out);
-    hipMemcpy(o, out, 4096, hipMemcpyDeviceToHost);
-    last = 0;
-    for (int i = 0; i < 1024; ++i) if (o[i] != 0xEEEEEEEEu) last = i;
-    printf("size 16: first 8 dwords: %x %x %x %x %x %x %x %x; last written %d\n", o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], last);
+    for (int shift = 0; shift <= 2; shift += 2) {
+        probe<16><<<1, 64>>>(src, out, shift);
+        hipMemcpy(o, out, 4096, hipMemcpyDeviceToHost);
+        last = 0;
+        int bad = 0;
+        for (int i = 0; i < 1024; ++i) if (o[i] != 0xEEEEEEEEu) last = i;
+        for (int l = 0; l < 64; ++l)
+            for (int w = 0; w < 4; ++w) bad += o[4 * l + w] != (uint32_t)(shift + 4 * l + w);
+        printf("size 16, source shift %d dwords: first 8 dwords: %x %x %x %x %x %x %x %x; last written %d; wrong %d\n",
+               shift, o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], last, bad);
+    }
     return 0;
 }
