@@ -94,13 +94,16 @@ int timeout_ms() {
     const char* e = std::getenv("COCOA_COMM_TIMEOUT_MS");
     return e ? std::atoi(e) : 120000;
 }
-// Exchange timeout (COCOA_COMM_EXCHANGE_TIMEOUT_MS, default 0 = none): a
-// round's recv also waits for the other ranks' work -- the strict chain, rank
-// 0's relay, ranks that finish set_train / the compact layout at different
-// times -- which on C4-sized data can outlast any handshake-sized limit.
+// Exchange timeout (COCOA_COMM_EXCHANGE_TIMEOUT_MS, default 30 min; 0 = none):
+// a round's recv also waits for the other ranks' work -- the strict chain,
+// rank 0's relay, ranks that finish set_train / the compact layout at
+// different times -- which on C4-sized data can outlast any handshake-sized
+// limit, but a rank that hangs without closing its socket (a wedged GPU, a
+// stuck host) must still end the others with an error instead of blocking them
+// forever.
 int exchange_timeout_ms() {
     const char* e = std::getenv("COCOA_COMM_EXCHANGE_TIMEOUT_MS");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 30 * 60 * 1000;
 }
 
 timeval to_timeval(int ms) {

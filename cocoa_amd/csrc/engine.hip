@@ -140,9 +140,12 @@ struct cocoa_ctx {
     std::vector<int32_t> g_k0;        // first partition of each sub (+ K at the end)
     std::vector<int64_t> g_r0;        // first training row of each sub (+ n)
     std::vector<int64_t> g_t0;        // first test row of each sub (+ n_test)
-    DevBuf g_stage;                   // fast exchange: the other subs' sums, on subs[0]'s device
-    std::vector<hipEvent_t> g_ev;     // per sub: its sum (its part of the chain, or the total) is ready
-    std::vector<hipEvent_t> g_ev_cp;  // per sub: it has copied the total
+    std::vector<hipEvent_t> g_ev;     // per sub: its fold (strict: its part of the chain) is ready
+    std::vector<hipEvent_t> g_ev_rs;  // per sub (fast): its column slice of the total is reduced
+    std::vector<hipEvent_t> g_ev_cp;  // per sub: it has copied the total (strict) / the other slices (fast)
+    // as a member of a multi-device context (fast mode): slice r of the other
+    // members' folds, gathered for this member's part of the reduce-scatter
+    DevBuf x_stage;
     bool is_group() const { return !subs.empty(); }
     // rank exchange (cocoa_comm_init): owned; null = single rank / caller-driven
     cocoa::Comm* comm = nullptr;
@@ -309,12 +312,10 @@ struct cocoa_ctx {
             (void)hipSetDevice(subs[r]->device);
             if (r < g_ev.size() && g_ev[r]) (void)hipEventDestroy(g_ev[r]);
             if (r < g_ev_cp.size() && g_ev_cp[r]) (void)hipEventDestroy(g_ev_cp[r]);
+            if (r < g_ev_rs.size() && g_ev_rs[r]) (void)hipEventDestroy(g_ev_rs[r]);
             delete subs[r];
         }
-        if (!subs.empty()) {
-            (void)hipSetDevice(device);
-            g_stage.free();
-        }
+        if (!subs.empty()) (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (gstream) {
             (void)hipStreamSynchronize(gstream);
@@ -371,10 +372,10 @@ static void require(bool cond, int code, const std::string& msg) {
 }
 
 // multi-device contexts (cocoa_create_multi): the group side of the entry points
-static void group_set_train(cocoa_ctx* g, int32_t K, const int64_t* part_ptr, const int64_t* row_ptr,
+static void group_set_train(cocoa_ctx* g, bool dense, int32_t K, const int64_t* part_ptr, const int64_t* row_ptr,
                             const int32_t* col, const double* val, const double* y, int64_t n, int32_t d,
                             int32_t part_begin, int32_t Kg);
-static void group_set_test(cocoa_ctx* g, const int64_t* row_ptr, const int32_t* col, const double* val,
+static void group_set_test(cocoa_ctx* g, bool dense, const int64_t* row_ptr, const int32_t* col, const double* val,
                            const double* y, int64_t n_rows);
 static void group_init(cocoa_ctx* g, const cocoa_params* params, const cocoa_debug* debug, int method,
                        const double* w_init);
@@ -522,11 +523,11 @@ static bool is_dense(const int64_t* row_ptr, const int32_t* col, int64_t n, int3
     return true;
 }
 
-static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const int64_t* row_ptr,
-                           const int32_t* col, const double* val, const double* y, int64_t n_rows,
-                           int32_t num_features, int32_t part_begin, int32_t num_parts_global);
-static void set_test_impl(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t* col, const double* val,
-                          const double* y, int64_t n_rows);
+static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, const int64_t* part_ptr,
+                           const int64_t* row_ptr, const int32_t* col, const double* val, const double* y,
+                           int64_t n_rows, int32_t num_features, int32_t part_begin, int32_t num_parts_global);
+static void set_test_impl(cocoa_ctx* ctx, bool dense_in, const int64_t* row_ptr, const int32_t* col,
+                          const double* val, const double* y, int64_t n_rows);
 
 // Compact deltaW layout (see cocoa_ctx::compact_ready).  COCOA_DW_COMPACT=0 / 1
 // forces it off / on (tests); on by default once K_loc * d * 8 >= 1 GiB and the
@@ -597,13 +598,13 @@ extern "C" int cocoa_set_train_dense(cocoa_ctx* ctx, int32_t num_parts, const in
     }
     CAPI_BEGIN(ctx)
     if (ctx->is_group()) {
-        group_set_train(ctx, num_parts, part_ptr, nullptr, nullptr, X, y, n_rows, num_features, part_begin,
+        group_set_train(ctx, true, num_parts, part_ptr, nullptr, nullptr, X, y, n_rows, num_features, part_begin,
                         num_parts_global);
         return COCOA_OK;
     }
     std::vector<int64_t> rp((size_t)n_rows + 1);
     for (int64_t r = 0; r <= n_rows; ++r) rp[(size_t)r] = r * (int64_t)num_features;
-    set_train_impl(ctx, num_parts, part_ptr, rp.data(), nullptr, X, y, n_rows, num_features, part_begin,
+    set_train_impl(ctx, true, num_parts, part_ptr, rp.data(), nullptr, X, y, n_rows, num_features, part_begin,
                    num_parts_global);
     CAPI_END(ctx)
 }
@@ -617,12 +618,12 @@ extern "C" int cocoa_set_test_dense(cocoa_ctx* ctx, const double* X, const doubl
     }
     CAPI_BEGIN(ctx)
     if (ctx->is_group()) {
-        group_set_test(ctx, nullptr, nullptr, X, y, n_rows);
+        group_set_test(ctx, true, nullptr, nullptr, X, y, n_rows);
         return COCOA_OK;
     }
     std::vector<int64_t> rp((size_t)n_rows + 1);
     for (int64_t r = 0; r <= n_rows; ++r) rp[(size_t)r] = r * (int64_t)ctx->d;
-    set_test_impl(ctx, rp.data(), nullptr, X, y, n_rows);
+    set_test_impl(ctx, true, rp.data(), nullptr, X, y, n_rows);
     CAPI_END(ctx)
 }
 
@@ -632,22 +633,25 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
     CAPI_BEGIN(ctx)
     require(col != nullptr || (row_ptr && n_rows >= 0 && row_ptr[n_rows] == 0), COCOA_E_ARG,
             "cocoa_set_train: null column array");
+    // a CSR whose rows are all empty may pass col == NULL: it stays CSR (the
+    // dense layout is selected only by cocoa_set_train_dense)
+    static const int32_t no_col = 0;
+    if (!col) col = &no_col;
     if (ctx->is_group()) {
-        static const int32_t no_col = 0;  // CSR (possibly empty), not the dense marker
-        group_set_train(ctx, num_parts, part_ptr, row_ptr, col ? col : &no_col, val, y, n_rows, num_features,
-                        part_begin, num_parts_global);
+        group_set_train(ctx, false, num_parts, part_ptr, row_ptr, col, val, y, n_rows, num_features, part_begin,
+                        num_parts_global);
         return COCOA_OK;
     }
-    set_train_impl(ctx, num_parts, part_ptr, row_ptr, col, val, y, n_rows, num_features, part_begin,
+    set_train_impl(ctx, false, num_parts, part_ptr, row_ptr, col, val, y, n_rows, num_features, part_begin,
                    num_parts_global);
     CAPI_END(ctx)
 }
 
-// col == nullptr: dense rows (row r = columns 0..d-1 at entries [r d, (r+1) d))
-static void set_train_impl(cocoa_ctx* ctx, int32_t num_parts, const int64_t* part_ptr, const int64_t* row_ptr,
-                           const int32_t* col, const double* val, const double* y, int64_t n_rows,
-                           int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
-    const bool dense_in = col == nullptr;
+// dense_in: dense rows (row r = columns 0..d-1 at entries [r d, (r+1) d), col unused)
+static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, const int64_t* part_ptr,
+                           const int64_t* row_ptr, const int32_t* col, const double* val, const double* y,
+                           int64_t n_rows, int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
+    require(dense_in || col != nullptr, COCOA_E_ARG, "cocoa_set_train: null column array");
     ctx->gram_quiesce();  // a Gram prefetch reads the CSR being replaced
     ctx->eval_quiesce();  // so does a pending evaluation
     require(num_parts >= 1 && part_ptr && row_ptr && y && n_rows >= 0 && num_features >= 1, COCOA_E_ARG,
@@ -808,19 +812,20 @@ extern "C" int cocoa_set_test(cocoa_ctx* ctx, const int64_t* row_ptr, const int3
     CAPI_BEGIN(ctx)
     require(col != nullptr || (row_ptr && n_rows >= 0 && row_ptr[n_rows] == 0), COCOA_E_ARG,
             "cocoa_set_test: null column array");
+    static const int32_t no_col = 0;  // all-empty CSR with col == NULL: still CSR
+    if (!col) col = &no_col;
     if (ctx->is_group()) {
-        static const int32_t no_col = 0;
-        group_set_test(ctx, row_ptr, col ? col : &no_col, val, y, n_rows);
+        group_set_test(ctx, false, row_ptr, col, val, y, n_rows);
         return COCOA_OK;
     }
-    set_test_impl(ctx, row_ptr, col, val, y, n_rows);
+    set_test_impl(ctx, false, row_ptr, col, val, y, n_rows);
     CAPI_END(ctx)
 }
 
-// col == nullptr: dense rows
-static void set_test_impl(cocoa_ctx* ctx, const int64_t* row_ptr, const int32_t* col, const double* val,
-                          const double* y, int64_t n_rows) {
-    const bool dense_in = col == nullptr;
+// dense_in: dense rows (col unused)
+static void set_test_impl(cocoa_ctx* ctx, bool dense_in, const int64_t* row_ptr, const int32_t* col,
+                          const double* val, const double* y, int64_t n_rows) {
+    require(dense_in || col != nullptr, COCOA_E_ARG, "cocoa_set_test: null column array");
     ctx->eval_quiesce();  // a pending evaluation reads the test rows being replaced
     require(ctx->d > 0, COCOA_E_STATE, "cocoa_set_test: call cocoa_set_train first");
     require(row_ptr && y && n_rows >= 0, COCOA_E_ARG, "cocoa_set_test: bad argument");
@@ -1750,7 +1755,9 @@ extern "C" int cocoa_eval_wait(cocoa_ctx* ctx, cocoa_eval_result* out) {
     eval_fire(ctx);  // no round was issued after cocoa_eval_async
     HIPCHK(hipEventSynchronize(ctx->e_done));
     ctx->eval_pending = false;
-    check_status(ctx);
+    // no check_status here: the next round's solver (enqueued before this
+    // evaluation fired) may still run on ctx->stream, so its status word is
+    // read by the next call that synchronises that stream (cocoa_sync / cocoa_eval)
     const double* h = ctx->h_eval + 4;
     finish(ctx, h[0], h[1], h[2], (int64_t)h[3], (int64_t)(ctx->has_test ? ctx->te.n : 0), out);
     CAPI_END(ctx)
@@ -2185,8 +2192,9 @@ extern "C" int cocoa_samples(cocoa_ctx* ctx, int32_t part, int32_t seed_plus_t, 
 // a multi-process run (same part_begin / num_parts_global, so sigma' = K gamma
 // and the scaling see the global K).  Per round every device runs its local
 // half on its own stream; the deltaW sums then meet on the devices' streams:
-//   fast   -- device 0 gathers the others' sums (peer copies over xGMI) and
-//             adds them in device order, every device copies the total;
+//   fast   -- a reduce-scatter then all-gather of column slices by peer
+//             copies over xGMI: device r sums slice r of every device's fold
+//             in device order, then every device copies the other slices;
 //   strict -- the ordered chain: device r's fold continues device r-1's (peer
 //             copy, then the fold kernel), the last device's total goes to all,
 // so strict stays bitwise equal to the single-device partition-order fold.
@@ -2226,6 +2234,9 @@ extern "C" int cocoa_create_multi(int32_t n_devices, const int32_t* devices, int
             g->g_ev.push_back(e1);
             HIPCHK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
             g->g_ev_cp.push_back(e2);
+            hipEvent_t e3 = nullptr;
+            HIPCHK(hipEventCreateWithFlags(&e3, hipEventDisableTiming));
+            g->g_ev_rs.push_back(e3);
         }
         g->device = g->subs[0]->device;
         // peer access between distinct devices (xGMI); copies work without it too
@@ -2259,12 +2270,11 @@ extern "C" int cocoa_num_devices(cocoa_ctx* ctx, int32_t* n_devices, int32_t* de
     CAPI_END(ctx)
 }
 
-// col == nullptr: dense rows (val = X[n][d])
-static void group_set_train(cocoa_ctx* g, int32_t K, const int64_t* part_ptr, const int64_t* row_ptr,
+// dense: dense rows (val = X[n][d], col unused)
+static void group_set_train(cocoa_ctx* g, bool dense, int32_t K, const int64_t* part_ptr, const int64_t* row_ptr,
                             const int32_t* col, const double* val, const double* y, int64_t n, int32_t d,
                             int32_t part_begin, int32_t Kg) {
     const int32_t N = (int32_t)g->subs.size();
-    const bool dense = col == nullptr;
     require(part_begin == 0 && Kg == K, COCOA_E_ARG,
             "a multi-device context holds the whole problem (part_begin = 0, num_parts_global = num_parts)");
     require(K >= N, COCOA_E_ARG, "cocoa_set_train: fewer partitions than devices");
@@ -2316,10 +2326,9 @@ static void group_set_train(cocoa_ctx* g, int32_t K, const int64_t* part_ptr, co
     g->inited = false;
 }
 
-static void group_set_test(cocoa_ctx* g, const int64_t* row_ptr, const int32_t* col, const double* val,
+static void group_set_test(cocoa_ctx* g, bool dense, const int64_t* row_ptr, const int32_t* col, const double* val,
                            const double* y, int64_t n_rows) {
     const int32_t N = (int32_t)g->subs.size();
-    const bool dense = col == nullptr;
     require(g->d > 0, COCOA_E_STATE, "cocoa_set_test: call cocoa_set_train first");
     require(y && n_rows >= 0 && (dense || row_ptr), COCOA_E_ARG, "cocoa_set_test: bad argument");
     if (!dense) require(row_ptr[0] == 0, COCOA_E_ARG, "row_ptr[0] must be 0");
@@ -2342,6 +2351,11 @@ static void group_set_test(cocoa_ctx* g, const int64_t* row_ptr, const int32_t* 
     g->te.n = n_rows;
 }
 
+// fast exchange: member r reduces the columns [slice(r), slice(r+1)) of deltaW
+static int64_t group_slice(const cocoa_ctx* g, size_t r) {
+    return (int64_t)g->d * (int64_t)r / (int64_t)g->subs.size();
+}
+
 static void group_init(cocoa_ctx* g, const cocoa_params* params, const cocoa_debug* debug, int method,
                        const double* w_init) {
     require(params && method >= 0 && method <= 4, COCOA_E_ARG, "cocoa_init: bad argument");
@@ -2354,7 +2368,14 @@ static void group_init(cocoa_ctx* g, const cocoa_params* params, const cocoa_deb
     g->scaling = g->subs[0]->scaling;
     g->alpha_oob = false;
     const size_t N = g->subs.size();
-    if (!g->strict && N > 1) g->g_stage.alloc(sizeof(double) * (N - 1) * (size_t)g->d);
+    if (!g->strict && N > 1)
+        for (size_t r = 0; r < N; ++r) {
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipSetDevice(sub->device));
+            const int64_t len = group_slice(g, r + 1) - group_slice(g, r);
+            sub->x_stage.alloc(sizeof(double) * (N - 1) * (size_t)std::max<int64_t>(len, 1));
+        }
+    HIPCHK(hipSetDevice(g->device));
     g->inited = true;
 }
 
@@ -2377,7 +2398,7 @@ static void group_round(cocoa_ctx* g, int32_t t) {
     require(g->inited, COCOA_E_STATE, "cocoa_round: call cocoa_init first");
     const size_t N = g->subs.size();
     const size_t bytes = sizeof(double) * (size_t)g->d;
-    size_t owner = 0;  // the device whose dw_sum ends up holding the total
+    size_t owner = 0;  // strict: the device whose dw_sum ends up holding the total
     if (N == 1) {
         HIPCHK(hipSetDevice(g->subs[0]->device));
         run_local(g->subs[0], t, true);
@@ -2397,25 +2418,65 @@ static void group_round(cocoa_ctx* g, int32_t t) {
         }
         owner = N - 1;
     } else {
+        // Every member folds its partitions; then a reduce-scatter and an
+        // all-gather of column slices, all on the members' own streams: member
+        // r gathers slice r of every other member's fold (N - 1 peer copies of
+        // d / N doubles over xGMI) and sums the N pieces in member order,
+        // ((x_0 + x_1) + x_2) + ..., the association the earlier gather-to-one
+        // exchange used, so the total is reproducible and bitwise identical on
+        // every member; then every member copies the other slices.  Per member
+        // 2 (N - 1) / N * 8 d bytes cross the links, all members at once.
         for (size_t r = 0; r < N; ++r) {
             cocoa_ctx* sub = g->subs[r];
             HIPCHK(hipSetDevice(sub->device));
             run_local(sub, t, false);
             HIPCHK(hipEventRecord(g->g_ev[r], sub->stream));
         }
-        // device 0: ((x_0 + x_1) + x_2) + ... in device order
-        cocoa_ctx* s0 = g->subs[0];
-        HIPCHK(hipSetDevice(s0->device));
-        double* stage = g->g_stage.as<double>();
-        for (size_t r = 1; r < N; ++r) {
+        for (size_t r = 0; r < N; ++r) {  // reduce-scatter
             cocoa_ctx* sub = g->subs[r];
-            HIPCHK(hipStreamWaitEvent(s0->stream, g->g_ev[r], 0));
-            HIPCHK(hipMemcpyPeerAsync(stage + (r - 1) * (size_t)g->d, s0->device, sub->dw_sum, sub->device, bytes,
-                                      s0->stream));
+            HIPCHK(hipSetDevice(sub->device));
+            const int64_t j0 = group_slice(g, r), len = group_slice(g, r + 1) - j0;
+            double* stage = sub->x_stage.as<double>();
+            for (size_t q = 0, i = 0; q < N; ++q) {
+                if (q == r) continue;
+                HIPCHK(hipStreamWaitEvent(sub->stream, g->g_ev[q], 0));
+                if (len > 0)
+                    HIPCHK(hipMemcpyPeerAsync(stage + i * (size_t)len, sub->device, g->subs[q]->dw_sum + j0,
+                                              g->subs[q]->device, sizeof(double) * (size_t)len, sub->stream));
+                ++i;
+            }
+            sub->timed(COCOA_K_FOLD, [&] {
+                launch_sum_slices(sub->dw_sum + j0, stage, (int32_t)N, (int32_t)r, len, sub->stream);
+            });
+            HIPCHK(hipEventRecord(g->g_ev_rs[r], sub->stream));
         }
-        s0->timed(COCOA_K_FOLD, [&] { launch_sum_into(s0->dw_sum, stage, (int32_t)(N - 1), g->d, s0->stream); });
-        HIPCHK(hipEventRecord(g->g_ev[0], s0->stream));
-        owner = 0;
+        for (size_t r = 0; r < N; ++r) {  // all-gather, then w += sum * scaling (CoCoA.scala:48)
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipSetDevice(sub->device));
+            for (size_t q = 0; q < N; ++q) {
+                if (q == r) continue;
+                const int64_t j0 = group_slice(g, q), len = group_slice(g, q + 1) - j0;
+                HIPCHK(hipStreamWaitEvent(sub->stream, g->g_ev_rs[q], 0));
+                if (len > 0)
+                    HIPCHK(hipMemcpyPeerAsync(sub->dw_sum + j0, sub->device, g->subs[q]->dw_sum + j0,
+                                              g->subs[q]->device, sizeof(double) * (size_t)len, sub->stream));
+            }
+            HIPCHK(hipEventRecord(g->g_ev_cp[r], sub->stream));
+            sub->timed(COCOA_K_APPLY, [&] {
+                launch_apply(sub->w.as<double>(), sub->dw_sum, sub->d, sub->mult, sub->d_inv.as<int32_t>(), sub->stream);
+            });
+            sub->xw_cached = false;
+        }
+        // a member's next fold overwrites its sum: only after every other
+        // member has copied its slice of it
+        for (size_t r = 0; r < N; ++r) {
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipSetDevice(sub->device));
+            for (size_t q = 0; q < N; ++q)
+                if (q != r) HIPCHK(hipStreamWaitEvent(sub->stream, g->g_ev_cp[q], 0));
+        }
+        HIPCHK(hipSetDevice(g->device));
+        return;
     }
     cocoa_ctx* src = g->subs[owner];
     for (size_t r = 0; r < N; ++r) {

@@ -246,7 +246,7 @@ void launch_sampler(const int64_t* part_ptr, int32_t K, int32_t seed, int32_t H,
 // original order, the order ranks exchange it in
 void launch_zero(double* p, int64_t n, int blocks, hipStream_t s);
 void launch_dense_cols(int32_t* col, uint16_t* col16, int64_t nnz, int32_t d, hipStream_t s);
-void launch_sum_into(double* dst, const double* stage, int32_t m, int64_t d, hipStream_t s);
+void launch_sum_slices(double* own, const double* stage, int32_t n, int32_t r, int64_t len, hipStream_t s);
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
                  const int32_t* inv, bool zero, hipStream_t s, const double* init = nullptr);
 // compact deltaW slices: column j's sum is the gather of dw[fpos[fptr[j] ..

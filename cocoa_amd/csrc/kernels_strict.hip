@@ -174,19 +174,25 @@ __global__ __launch_bounds__(256) void dense_cols_kernel(int32_t* col, uint16_t*
     }
 }
 
-// dst[j] = ((dst[j] + stage[0][j]) + stage[1][j]) + ... : the multi-device
-// context's fast exchange, the other devices' sums added in device order
-__global__ __launch_bounds__(256) void sum_into_kernel(double* dst, const double* stage, int32_t m, int64_t d) {
-    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < d; j += (int64_t)gridDim.x * 256) {
-        double acc = dst[j];
-        for (int32_t r = 0; r < m; ++r) acc = acc + stage[(size_t)r * (size_t)d + (size_t)j];
-        dst[j] = acc;
+// The multi-device context's fast exchange, member r's part of the
+// reduce-scatter: own[j] = ((x_0[j] + x_1[j]) + x_2[j]) + ... over the n
+// members in member order, where x_r is own itself and the others' pieces sit
+// in stage[0 .. n-2] (member q at q, or q-1 past r), len doubles each.
+__global__ __launch_bounds__(256) void sum_slices_kernel(double* own, const double* stage, int32_t n, int32_t r,
+                                                         int64_t len) {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < len; j += (int64_t)gridDim.x * 256) {
+        double acc = 0.0;
+        for (int32_t q = 0; q < n; ++q) {
+            const double v = q == r ? own[j] : stage[(size_t)(q < r ? q : q - 1) * (size_t)len + (size_t)j];
+            acc = q == 0 ? v : acc + v;
+        }
+        own[j] = acc;
     }
 }
 
-void launch_sum_into(double* dst, const double* stage, int32_t m, int64_t d, hipStream_t s) {
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((d + 255) / 256, 2048));
-    if (m > 0 && d > 0) sum_into_kernel<<<blocks, 256, 0, s>>>(dst, stage, m, d);
+void launch_sum_slices(double* own, const double* stage, int32_t n, int32_t r, int64_t len, hipStream_t s) {
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((len + 255) / 256, 2048));
+    if (n > 1 && len > 0) sum_slices_kernel<<<blocks, 256, 0, s>>>(own, stage, n, r, len);
 }
 
 void launch_dense_cols(int32_t* col, uint16_t* col16, int64_t nnz, int32_t d, hipStream_t s) {

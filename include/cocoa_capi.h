@@ -14,13 +14,17 @@
  * Ownership: the caller owns every host buffer it passes; the engine copies
  * inputs to device memory and copies results out.  A context owns its device
  * memory, its HIP stream and its communicator; it is not thread-safe and is
- * driven from one host thread.  Multi-GPU = one process (and one context) per
- * GPU: rank 0 makes a communicator id (cocoa_comm_unique_id), the caller hands
- * the 128 bytes to every rank by any means (a file, its own RPC, MPI, ...),
- * every rank calls cocoa_comm_init, and from then on cocoa_round /
- * cocoa_eval / cocoa_run exchange deltaW and the objective sums internally
- * (RCCL over xGMI).  cocoa_round_local() / cocoa_round_apply() remain for a
- * caller that does the exchange itself.
+ * driven from one host thread.  Multi-GPU comes in two shapes:
+ *   - one context over several GPUs in one process (cocoa_create_multi): the
+ *     shape of the reference's single driver JVM; the devices exchange deltaW
+ *     among themselves inside cocoa_round;
+ *   - one process (and one context) per GPU: rank 0 makes a communicator id
+ *     (cocoa_comm_unique_id), the caller hands the 128 bytes to every rank by
+ *     any means (a file, its own RPC, MPI, ...), every rank calls
+ *     cocoa_comm_init, and from then on cocoa_round / cocoa_eval / cocoa_run
+ *     exchange deltaW and the objective sums internally (RCCL over xGMI).
+ * cocoa_round_local() / cocoa_round_apply() remain for a caller that does the
+ * exchange itself.
  */
 #ifndef COCOA_CAPI_H
 #define COCOA_CAPI_H
@@ -102,8 +106,10 @@ int cocoa_create(int device, int strict, void *stream, cocoa_ctx **out);
  * cocoa_set_train's data (which must be the whole problem: part_begin 0,
  * num_parts_global = num_parts) and the test rows [n_t r / n, n_t (r+1) / n).
  * Every round the devices exchange deltaW on their own streams (peer copies over
- * xGMI; fast: an ordered sum on device 0, strict: the partition-order chain,
- * so strict results stay bitwise equal to one device); cocoa_eval merges the
+ * xGMI; fast: a reduce-scatter then all-gather of column slices, device r
+ * summing slice r of every device's fold in device order, so the result is
+ * reproducible and identical on every device; strict: the partition-order
+ * chain, so strict results stay bitwise equal to one device); cocoa_eval merges the
  * objective terms; w / alpha / checkpoints are those of the whole problem (a
  * checkpoint is interchangeable with a one-device context's).  The
  * caller-driven exchange entry points (cocoa_round_local, cocoa_round_apply,

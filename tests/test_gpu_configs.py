@@ -7,9 +7,10 @@ objectives of size ~0.1-1, the tolerance is taken relative to the primal:
 |gap - gap_ref| <= 1e-9 |P_ref|.  Problems are built by cocoa_amd.configs
 exactly as bench.py builds them (the same seeded generators).  Every line
 DESIGN.md publishes is parity-tested at the size it is benchmarked at: C2 /
-C5 at the full BASELINE size, C3 at n = 400,000 (and a 25,600-row cut for the
-quicker strict checks), C4 as the one-GPU K = 1,024 problem (and one GPU's
-strong-scaling share of the 8-GPU problem).
+C5 at the full BASELINE size, C3 at n = 400,000 for CoCoA+ and CoCoA (and a
+25,600-row cut for the quicker strict checks), C4 as the one-GPU K = 1,024
+problem (and one GPU's strong-scaling share of the 8-GPU problem); the 8-GPU
+splits of C3 and C4 run as one 8-member context (cocoa_create_multi).
 Reference: CoCoA.scala:148-188 (local SDCA), MinibatchCD.scala:95-125,
 SGD.scala:104-135, OptUtils.scala:57-98.
 """
@@ -274,13 +275,77 @@ def test_c3_full_fast_10_rounds_vs_oracle(c3_full):
     del e
 
 
-@pytest.mark.timeout(1200)
-def test_c4_one_gpu_k1024_fast_vs_oracle():
-    """The C4 one-GPU line: n = 2,396,130, d = 3,231,961, K = 1,024 on one
-    GPU (chain solver on compact deltaW slices), 3 rounds, exact error counts."""
+@pytest.mark.timeout(900)
+def test_c3_full_cocoa_strict_bitwise_vs_oracle(c3_full):
+    """C3's other half, CoCoA (plus = false): scaling beta/K (CoCoA.scala:37)
+    and the local solver updating the task's w in place (the alias,
+    CoCoA.scala:182-184), at the benchmarked n = 400,000, 2 rounds bitwise."""
+    sh, od, ot = c3_full
+    e = make_engine(sh, strict=True)
+    e.init("cocoa", sh.n_glob, 2, sh.H, sh.lam)
+    run = make_run(sh, od, "cocoa")
+    for t in (1, 2):
+        e.round(t)
+        run.round(t)
+    assert np.array_equal(e.w(), run.w())
+    assert np.array_equal(e.alpha(), run.alpha())
+    ev, rv = e.eval(), run.eval(ot)
+    assert ev["gap"].hex() == rv["gap"].hex()
+    assert ev["test_err_count"] == rv["test_err"]
+    del e
+
+
+@pytest.mark.timeout(900)
+def test_c3_full_cocoa_fast_10_rounds_vs_oracle(c3_full):
+    sh, od, ot = c3_full
+    e = make_engine(sh, strict=False)
+    e.init("cocoa", sh.n_glob, 10, sh.H, sh.lam)
+    assert e.plan()["solver"] == "dense"
+    run = make_run(sh, od, "cocoa")
+    for t in range(1, 11):
+        e.round(t)
+        run.round(t)
+        if t % 5 == 0:
+            assert_close(e.eval(), run.eval(ot), True, t)
+    assert_state_close(e, run, True)
+    del e
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa"])
+def test_c3_full_eight_member_context_fast_vs_oracle(c3_full, method):
+    """C3's 8-GPU split as ONE context over 8 members (cocoa_create_multi; the
+    one-GPU pool repeats ordinal 0): 8 partitions per member, the 16 KB deltaW
+    reduce-scatter + all-gather every round (CoCoA.scala:45-48), 5 rounds."""
+    sh, od, ot = c3_full
+    e = Engine(devices=[0] * 8, strict=False)
+    e.set_train(sh.train)
+    e.set_test(sh.test)
+    e.init(method, sh.n_glob, 5, sh.H, sh.lam)
+    plan = e.plan()
+    assert plan["solver"] == "dense" and plan["n_devices"] == 8, plan
+    run = make_run(sh, od, method)
+    for t in range(1, 6):
+        e.round(t)
+        run.round(t)
+    assert_close(e.eval(), run.eval(ot), True, 5)
+    assert_state_close(e, run, True)
+    del e
+
+
+@pytest.fixture(scope="module")
+def c4_full():
+    # the C4 problem: n = 2,396,130, d = 3,231,961, K = 1,024
     sh = configs.share("c4", n_test=20000)
     assert sh.k_glob == 1024 and sh.train.num_parts == 1024
-    od, ot = odata(sh.train), odata(sh.test)
+    return sh, odata(sh.train), odata(sh.test)
+
+
+@pytest.mark.timeout(1200)
+def test_c4_one_gpu_k1024_fast_vs_oracle(c4_full):
+    """The C4 one-GPU line: n = 2,396,130, d = 3,231,961, K = 1,024 on one
+    GPU (chain solver on compact deltaW slices), 3 rounds, exact error counts."""
+    sh, od, ot = c4_full
     e = make_engine(sh, strict=False)
     e.init("cocoa+", sh.n_glob, 3, sh.H, sh.lam)
     plan = e.plan()
@@ -291,3 +356,26 @@ def test_c4_one_gpu_k1024_fast_vs_oracle():
         run.round(t)
     assert_close(e.eval(), run.eval(ot), True, 3)
     assert_state_close(e, run, True)
+    del e
+
+
+@pytest.mark.timeout(1200)
+def test_c4_eight_member_context_fast_vs_oracle(c4_full):
+    """C4's "deltaW all-reduce on 8 GPUs" shape as ONE context over 8 members:
+    128 partitions each (Gram-window solvers on compact slices), the 25.9 MB
+    deltaW reduce-scatter + all-gather every round, 2 rounds against the
+    oracle's single-process partition-order run."""
+    sh, od, ot = c4_full
+    e = Engine(devices=[0] * 8, strict=False)
+    e.set_train(sh.train)
+    e.set_test(sh.test)
+    e.init("cocoa+", sh.n_glob, 2, sh.H, sh.lam)
+    plan = e.plan()
+    assert plan["n_devices"] == 8 and plan["dw_compact"] == 1, plan
+    run = make_run(sh, od, "cocoa+")
+    for t in (1, 2):
+        e.round(t)
+        run.round(t)
+    assert_close(e.eval(), run.eval(ot), True, 2)
+    assert_state_close(e, run, True)
+    del e

@@ -191,3 +191,66 @@ def test_caller_driven_exchange_is_rejected(c1):
     g.round(1)
     ks = g.kernel_stats()
     assert ks["solver"]["launches"] == 2  # one solver launch per device
+
+
+def _tiny(d, n=48, K=4, seed=7):
+    """n rows over d features (d may be below the member count: some members'
+    column slices of the exchange are then empty)."""
+    from cocoa_amd.data import LabeledData
+    rng = np.random.default_rng(seed)
+    cols, vals, rp = [], [], [0]
+    for _ in range(n):
+        z = int(rng.integers(0, d + 1))
+        c = np.sort(rng.choice(d, size=z, replace=False)).astype(np.int32)
+        cols.append(c)
+        vals.append(rng.standard_normal(z))
+        rp.append(rp[-1] + z)
+    y = np.where(rng.random(n) < 0.5, 1.0, -1.0)
+    pp = np.array([(n * k) // K for k in range(K + 1)], np.int64)
+    return LabeledData(np.array(rp, np.int64), np.concatenate(cols).astype(np.int32), np.concatenate(vals), y, pp, d)
+
+
+@pytest.mark.parametrize("strict", [True, False])
+def test_fewer_features_than_members(strict):
+    """d = 3 over 4 members: member 0's slice of the fast exchange is empty."""
+    tr = _tiny(3)
+    od = odata(tr)
+    e = Engine(devices=[0] * 4, strict=strict)
+    e.set_train(tr)
+    e.set_test(tr)
+    e.init("cocoa+", tr.n, 5, 10, 1e-2)
+    run = oracle.Run(od, "cocoa+", tr.n, 10, 1e-2)
+    for t in range(1, 6):
+        e.round(t)
+        run.round(t)
+    wr = run.w()
+    if strict:
+        assert np.array_equal(e.w(), wr) and np.array_equal(e.alpha(), run.alpha())
+    else:
+        assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+    ev, rv = e.eval(), run.eval(od)
+    assert ev["test_err_count"] == rv["test_err"]
+
+
+@pytest.mark.parametrize("n_dev", [None, 2])
+def test_null_column_array_with_empty_rows(n_dev):
+    """cocoa_set_train / cocoa_set_test with col == NULL and every
+    row empty is an (empty) CSR, not the dense layout; init, round and eval run
+    and match the oracle (all-zero rows leave w = 0 and alpha = 0)."""
+    from cocoa_amd import _capi as C
+    n, d, K = 8, 5, 2
+    rp = np.zeros(n + 1, np.int64)
+    pp = np.array([0, 4, 8], np.int64)
+    y = np.array([1, -1, 1, 1, -1, -1, 1, -1], np.float64)
+    e = Engine(strict=False) if n_dev is None else Engine(devices=[0] * n_dev, strict=False)
+    lib = C.lib()
+    C.check(lib.cocoa_set_train(e.h, K, C.i64p(pp), C.i64p(rp), None, None, C.f64p(y), n, d, 0, K), e.h)
+    e.d, e.n_rows, e.K_loc, e.K_glob, e.part_begin = d, n, K, K, 0
+    C.check(lib.cocoa_set_test(e.h, C.i64p(rp), None, None, C.f64p(y), n), e.h)
+    assert e.plan()["solver"] != "dense"
+    e.init("cocoa+", n, 2, 3, 1e-2)
+    e.round(1)
+    e.round(2)
+    ev = e.eval()
+    assert np.array_equal(e.w(), np.zeros(d))
+    assert ev["primal"] == 1.0 and ev["test_err_count"] == n  # hinge 1 on every row; x.w = 0 is an error
