@@ -38,18 +38,38 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def solver_bytes_per_round(tr, H, seed_t, plus=True):
-    """Algorithmic bytes of one solver launch:
-    per coordinate step 16 (row_ptr pair) + 8 (y) + 16 (alpha r/w) + 36*z
-    (12 B CSR entry + w gather + deltaW gather + deltaW write) for CoCoA+."""
+def solver_bytes_per_round(tr, H, seed_t, method="cocoa+", solver="gram"):
+    """Algorithmic bytes of one solver launch (DESIGN.md
+    section 3 table), per coordinate step of a sampled row with z entries:
+      sparse SDCA (gram / chain): 16 (row_ptr pair) + 8 (y) + 16 (alpha r/w)
+        + 36 z (12 B CSR entry + w gather + deltaW gather + deltaW write) for
+        CoCoA+ / MbCD, 44 z for CoCoA (its task-local w is read and written too);
+      dense rows (dense solver): 8 d (the row) + 20 (sample, y, ||x||^2) -- w and
+        deltaW stay in registers, no gathers;
+      mb-SGD: 16 + 8 + 20 z (entry + w gather); local SGD: 16 + 8 + 36 z."""
     import cocoa_amd
+    K = tr.num_parts
+    if solver == "dense":
+        return K * H * (8 * tr.num_features + 20)
     z = np.diff(tr.row_ptr)
+    per_step, per_entry = {"cocoa+": (40, 36), "mbcd": (40, 36), "cocoa": (40, 44),
+                           "mbsgd": (24, 20), "localsgd": (24, 36)}[method]
     tot = 0
-    for k in range(tr.num_parts):
+    for k in range(K):
         p0, p1 = int(tr.part_ptr[k]), int(tr.part_ptr[k + 1])
         idx = cocoa_amd.jrandom_ints(seed_t, p1 - p0, H)
-        tot += 40 * H + (36 if plus else 44) * int(z[p0 + idx].sum())
+        tot += per_step * H + per_entry * int(z[p0 + idx].sum())
     return tot
+
+
+def eval_bytes(tr, te, d, dense):
+    """Algorithmic bytes of one evaluation pass (OptUtils.scala:57-98): every
+    train and test entry once, y, alpha, w; CSR rows 12 B per entry plus the row
+    pointers, dense rows (X[n][d], no column indices) 8 B per entry."""
+    if dense:
+        return 8 * tr.n * d + 8 * tr.n + 8 * tr.n + 8 * d + 8 * te.n * d + 8 * te.n
+    return (12 * tr.nnz + 8 * (tr.n + 1) + 8 * tr.n + 8 * tr.n + 8 * d
+            + 12 * te.nnz + 8 * (te.n + 1) + 8 * te.n)
 
 
 def main():
@@ -212,14 +232,11 @@ def main():
         log(f"gap {final_gap:.3g} after {rounds[-1]} rounds, {ttg:.3f}s")
 
     # ---- roofline of the dominant kernel (solver) and of the eval pass -----
+    plan = eng.plan()
     solver_ms = stats["solver"]["total_ms"] / max(stats["solver"]["launches"], 1)
-    b_solver = np.mean([solver_bytes_per_round(tr, H, t_ + 0, plus=args.method != "cocoa")
+    b_solver = np.mean([solver_bytes_per_round(tr, H, t_ + 0, args.method, plan.get("solver", "gram"))
                         for t_ in timed_rounds[:4]])
     ach = b_solver / (solver_ms * 1e-3) / 1e9
-    # HBM traffic per launch from the committed PMC passes (tools/gpu_pmc.sh ->
-    # tools/pmc_summary.py -> profiles/traffic.json), used only when the PMC run
-    # profiled the same kernel variant this run launched
-    plan = eng.plan()
     # HBM traffic per launch from the committed PMC passes, only for the kernels
     # this run launched (fast mode, the C2 headline workload the passes profiled)
     traffic = traffic_eval = None
@@ -233,10 +250,12 @@ def main():
             traffic_eval = rec["hbm_bytes_per_launch"] if rec else None
         except Exception:
             traffic = traffic_eval = None
-    eval_overlapped_ms = stats["eval"]["total_ms"] / max(stats["eval"]["launches"], 1)
-    eval_ms = eval_alone.get("total_ms", 0.0) / max(eval_alone.get("launches", 0), 1) if eval_alone else eval_overlapped_ms
-    b_eval = (12 * tr.nnz + 8 * (tr.n + 1) + 8 * tr.n + 8 * tr.n + 8 * args.d
-              + 12 * te.nnz + 8 * (te.n + 1) + 8 * te.n)
+    # the eval's launch average over the timed region (HIP events on the
+    # engine's stream); the 5 launches after it, with nothing beside them, are
+    # reported as alone_ms
+    eval_ms = stats["eval"]["total_ms"] / max(stats["eval"]["launches"], 1)
+    eval_alone_ms = (eval_alone.get("total_ms", 0.0) / max(eval_alone.get("launches", 0), 1)) if eval_alone else None
+    b_eval = eval_bytes(tr, te, args.d, plan.get("solver") == "dense")
     ach_eval = b_eval / (eval_ms * 1e-3) / 1e9
 
     # ---- CPU baseline: the oracle on this box's host cores (rank 0, N=1) ---
@@ -253,40 +272,51 @@ def main():
             naff = len(os.sched_getaffinity(0))
         except (AttributeError, OSError):
             naff = ncpu
-        cores = max(1, min(tr.num_parts, ncpu))
         od = oracle.Data(tr.row_ptr, tr.col, tr.val, tr.y, tr.part_ptr, tr.num_features)
         ot = oracle.Data(te.row_ptr, te.col, te.val, te.y, te.part_ptr, te.num_features)
-        run = oracle.Run(od, args.method, n_glob, H, args.lam, nthreads=cores)
-        run.set_global_parts(K_glob)
-        t_round = t_eval = 0.0
-        rounds = 0
-        cpu_gap = None
-        cpu_ttg = None
-        tc0 = time.perf_counter()
-        for r in range(1, args.gap_max_rounds + 1):
-            tc = time.perf_counter()
-            run.round(r)
-            t_round += time.perf_counter() - tc
-            rounds = r
-            if sdca:
+
+        def cpu_run(cores):
+            run = oracle.Run(od, args.method, n_glob, H, args.lam, nthreads=cores)
+            run.set_global_parts(K_glob)
+            t_round = t_eval = 0.0
+            rounds = 0
+            cpu_gap = cpu_ttg = None
+            tc0 = time.perf_counter()
+            for r in range(1, args.gap_max_rounds + 1):
                 tc = time.perf_counter()
-                cpu_gap = run.eval(ot)["gap"]
-                t_eval += time.perf_counter() - tc
-                if not args.no_gap and cpu_gap <= args.gap_target:
-                    cpu_ttg = time.perf_counter() - tc0
+                run.round(r)
+                t_round += time.perf_counter() - tc
+                rounds = r
+                if sdca:
+                    tc = time.perf_counter()
+                    cpu_gap = run.eval(ot)["gap"]
+                    t_eval += time.perf_counter() - tc
+                    if not args.no_gap and cpu_gap <= args.gap_target:
+                        cpu_ttg = time.perf_counter() - tc0
+                        break
+                if time.perf_counter() - tc0 > args.cpu_seconds:
                     break
-            if time.perf_counter() - tc0 > args.cpu_seconds:
-                break
-        ups = tr.num_parts * H * rounds / max(t_round, 1e-9)
-        cpu = {"value": ups, "unit": "coord updates/s", "cores": cores, "cpu_count": ncpu, "affinity_cpus": naff,
-               "kind": "port", "ms_per_round": t_round / rounds * 1e3,
-               "eval_ms": (t_eval / rounds * 1e3) if sdca else None,
-               "time_to_gap_s": cpu_ttg, "rounds": rounds, "final_gap": cpu_gap,
+            return {"value": tr.num_parts * H * rounds / max(t_round, 1e-9), "cores": cores,
+                    "ms_per_round": t_round / rounds * 1e3, "eval_ms": (t_eval / rounds * 1e3) if sdca else None,
+                    "time_to_gap_s": cpu_ttg, "rounds": rounds, "final_gap": cpu_gap,
+                    "stopped_s": time.perf_counter() - tc0}
+
+        cores = max(1, min(tr.num_parts, ncpu))
+        c = cpu_run(cores)
+        # the one-GPU job's fair share of a shared 8-GPU host's cores (16 on the
+        # GPU boxes, where os.cpu_count() reports the whole machine)
+        fair = cpu_run(min(16, cores)) if cores > 16 else None
+        cpu = {"value": c["value"], "unit": "coord updates/s", "cores": cores, "cpu_count": ncpu, "affinity_cpus": naff,
+               "kind": "port", "ms_per_round": c["ms_per_round"], "eval_ms": c["eval_ms"],
+               "time_to_gap_s": c["time_to_gap_s"], "rounds": c["rounds"], "final_gap": c["final_gap"],
+               "fair_share_16": fair,
                "sample": f"fresh {args.method} run of the same {args.config.upper()} shard (K={tr.num_parts}, H={H}) by the strict C "
                          f"oracle (oracle/cocoa_oracle.c) as Spark local[{cores}]: {cores} threads, one task per partition, "
-                         f"ordered reduce, gap/test-error evaluation every round; {rounds} rounds, "
-                         + (f"gap {args.gap_target:g} reached in {cpu_ttg:.2f}s" if cpu_ttg is not None else
-                            f"stopped after {time.perf_counter() - tc0:.1f}s (--cpu-seconds) at gap {cpu_gap}")}
+                         f"ordered reduce, gap/test-error evaluation every round; {c['rounds']} rounds, "
+                         + (f"gap {args.gap_target:g} reached in {c['time_to_gap_s']:.2f}s" if c["time_to_gap_s"] is not None
+                            else f"stopped after {c['stopped_s']:.1f}s (--cpu-seconds) at gap {c['final_gap']}")
+                         + ("; fair_share_16: the same run on 16 threads (a one-GPU job's share of the host)"
+                            if fair else "")}
         log(f"cpu baseline {cpu}")
 
     if rank == 0:
@@ -299,6 +329,8 @@ def main():
             "vs_baseline": (value / cpu["value"]) if cpu else None,
             "vs_baseline_basis": "value / cpu_baseline.value (coord updates/s; no published number exists)" if cpu else None,
             "time_to_gap_vs_cpu": (cpu["time_to_gap_s"] / ttg) if (cpu and ttg and cpu.get("time_to_gap_s")) else None,
+            "time_to_gap_vs_cpu16": (cpu["fair_share_16"]["time_to_gap_s"] / ttg)
+            if (cpu and ttg and cpu.get("fair_share_16") and cpu["fair_share_16"].get("time_to_gap_s")) else None,
             "dtype": "f64",
             "data": cfg["data"],
             "config": {"workload": f"{args.config.upper()} {cfg['shape']} {args.method} (n={tr.n}/GPU of {n_glob}, d={args.d}, "
@@ -319,9 +351,10 @@ def main():
             "roofline_eval": {"kernel": "eval (primal/dual/gap/test error SpMV)", "bound": "hbm", "achieved": ach_eval,
                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach_eval / PEAK_HBM_GBS,
                               "traffic": traffic_eval, "bytes_per_launch": b_eval, "avg_launch_ms": eval_ms,
-                              "note": ("measured alone (5 launches after the timed region); in the timed loop the "
-                                       f"eval runs beside the next round's solver: {eval_overlapped_ms:.4f} ms")
-                              if pipe else "measured in the timed loop"},
+                              "alone_ms": eval_alone_ms,
+                              "note": "avg_launch_ms: HIP events over the timed rounds (beside the next round's "
+                                      "Gram rows on the side stream" + (" and solver, --pipeline)" if pipe else ")")
+                                      + "; alone_ms: 5 launches after the timed region with nothing beside them"},
             "kernel_ms": {k: (v["total_ms"] / max(v["launches"], 1)) for k, v in stats.items()},
             "cpu_baseline": cpu,
             "plan": plan,

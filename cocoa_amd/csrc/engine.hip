@@ -159,6 +159,7 @@ struct cocoa_ctx {
     // eval does not share HBM with it) and runs beside the latency-bound solver.
     DevBuf dw2;
     bool dw_dbuf = false;
+    int64_t dw_slice = 0;  // doubles per partition slice (d, or max_u for compact slices)
     hipStream_t zstream = nullptr;
     hipEvent_t zdone[2] = {nullptr, nullptr}, folded = nullptr;
     bool zpending[2] = {false, false};
@@ -917,7 +918,7 @@ static int reg_chunks_for(int64_t nnz, int64_t rows, int method) {
     return (mode == MODE_MBCD && rows > 0 && nnz <= 96 * rows) ? short_row_chunks(mode, false) : kRegChunks;
 }
 
-static bool dw_double_buffer(size_t bytes);
+static bool dw_double_buffer(size_t bytes, bool compact);
 
 extern "C" int cocoa_set_solver(cocoa_ctx* ctx, int kind) {
     CAPI_BEGIN(ctx)
@@ -984,17 +985,22 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     ctx->dw_compact = ctx->compact_ready && (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_MBCD) &&
                       params->local_iters >= 1 && !(ctx->tr_dense && dense_solver_fits(d, ctx->max_nl));
     const int64_t slice = ctx->dw_compact ? ctx->max_u : d;
+    ctx->dw_slice = slice;
     ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * slice), s);
     // a second deltaW set only when it fits next to everything else (with 1 GiB
-    // to spare); otherwise single buffering with the zero-in-fold path
-    ctx->dw_dbuf = !ctx->dw_compact && dw_double_buffer((size_t)(K * d) * sizeof(double));
+    // to spare); otherwise single buffering with the zero-in-fold path.  Compact
+    // slices (C4: 1,024 x 64,847 doubles, 0.53 GB a set) take the second set
+    // too: the fold then only reads, and the set it folded is re-zeroed by a
+    // streaming memset beside the next round's solver instead of by 62 M
+    // scattered 8-byte stores.
+    ctx->dw_dbuf = dw_double_buffer((size_t)(K * slice) * sizeof(double), ctx->dw_compact);
     if (ctx->dw_dbuf) {
         size_t free_b = 0, total_b = 0;
         HIPCHK(hipMemGetInfo(&free_b, &total_b));
-        if (free_b < sizeof(double) * (size_t)(K * d) + ((size_t)1 << 30)) ctx->dw_dbuf = false;
+        if (free_b < sizeof(double) * (size_t)(K * slice) + ((size_t)1 << 30)) ctx->dw_dbuf = false;
     }
     if (ctx->dw_dbuf) {
-        ctx->dw2.alloc_zero(sizeof(double) * (size_t)(K * d), s);
+        ctx->dw2.alloc_zero(sizeof(double) * (size_t)(K * slice), s);
         if (!ctx->zstream) {
             HIPCHK(hipStreamCreateWithFlags(&ctx->zstream, hipStreamNonBlocking));
             for (auto& e : ctx->zdone) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1143,10 +1149,10 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
 // K_loc * d * 8 >= 1 GiB (C4: 1,024 x 3.23 M doubles = 26.5 GB per set).
 // COCOA_DW_DBUF=0 / 1 forces it off / on (tests); cocoa_init still falls back
 // to one set when the second does not fit in device memory.
-static bool dw_double_buffer(size_t bytes) {
+static bool dw_double_buffer(size_t bytes, bool compact) {
     const char* e = std::getenv("COCOA_DW_DBUF");
     if (e) return std::atoi(e) != 0;
-    return bytes >= ((size_t)1 << 30);
+    return compact || bytes >= ((size_t)1 << 30);
 }
 
 static GramArgs gram_args(cocoa_ctx* c, const int32_t* samples, double* gt) {
@@ -1192,7 +1198,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         HIPCHK(hipStreamWaitEvent(c->zstream, c->folded, 0));
         // hipMemsetAsync: C4 22.8-23.3 ms/round; a narrow zero_kernel grid (64-128
         // workgroups) measured 23.0 (r01), so the plain memset stays
-        HIPCHK(hipMemsetAsync(zs, 0, sizeof(double) * (size_t)K * (size_t)d, c->zstream));
+        HIPCHK(hipMemsetAsync(zs, 0, sizeof(double) * (size_t)K * (size_t)c->dw_slice, c->zstream));
         HIPCHK(hipEventRecord(c->zdone[c->zero_owed], c->zstream));
         c->zpending[c->zero_owed] = true;
         c->zero_owed = -1;
@@ -1369,7 +1375,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
     c->timed(COCOA_K_FOLD, [&] {
         if (c->dw_compact)
             launch_fold_compact(dws, c->fptr.as<int64_t>(), c->fpos.as<uint32_t>(), d, c->dw_sum, c->w.as<double>(),
-                                c->mult, fuse_apply, c->d_inv.as<int32_t>(), s, chain_init);
+                                c->mult, fuse_apply, c->d_inv.as<int32_t>(), !c->dw_dbuf, s, chain_init);
         else
             launch_fold(dws, K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, c->d_inv.as<int32_t>(),
                         !c->dw_dbuf, s, chain_init);

@@ -252,7 +252,8 @@ void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double*
 // compact deltaW slices: column j's sum is the gather of dw[fpos[fptr[j] ..
 // fptr[j+1])] in partition order (each entry re-zeroed as it is read)
 void launch_fold_compact(double* dw, const int64_t* fptr, const uint32_t* fpos, int64_t d, double* dw_sum, double* w,
-                         double mult, bool apply, const int32_t* inv, hipStream_t s, const double* init = nullptr);
+                         double mult, bool apply, const int32_t* inv, bool zero, hipStream_t s,
+                         const double* init = nullptr);
 void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const int32_t* inv, hipStream_t s);
 void launch_scale(double* w, int64_t d, double scale, hipStream_t s);
 void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, double* out, hipStream_t s);

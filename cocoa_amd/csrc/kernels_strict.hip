@@ -97,13 +97,15 @@ void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double*
 
 // Fold of compact deltaW slices (C4 layout, cocoa_ctx::compact_ready): one
 // thread per device column j sums the slice entries that hold j in partition
-// order -- the dense fold's order with its zero terms dropped -- and zeroes
-// them for the next round.  Device order puts the columns every partition
+// order -- the dense fold's order with its zero terms dropped -- and, with a
+// single slice set, zeroes them for the next round (double-buffered sets are
+// re-zeroed by a streaming memset beside the next round's solver instead:
+// the scattered 8-byte zero stores cost a partial-line write each).  Device order puts the columns every partition
 // touches first, and a partition's slice lists its columns in device order,
 // so the threads of a wave read neighbouring positions of each slice.
 __global__ __launch_bounds__(256) void fold_compact_kernel(double* dw, const int64_t* fptr, const uint32_t* fpos,
                                                            int64_t d, double* dw_sum, double* w, double mult,
-                                                           int apply, const int32_t* inv, const double* init) {
+                                                           int apply, const int32_t* inv, const double* init, int zero) {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < d; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t jo = inv ? inv[j] : j;
         const int64_t b = fptr[j], e = fptr[j + 1];
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(256) void fold_compact_kernel(double* dw, const int
         if (q < e) {
             const uint32_t p = fpos[q++];
             s = init ? init[jo] + dw[p] : dw[p];
-            dw[p] = 0.0;
+            if (zero) dw[p] = 0.0;
         } else if (init) {
             s = init[jo];
         }
@@ -123,15 +125,17 @@ __global__ __launch_bounds__(256) void fold_compact_kernel(double* dw, const int
             s = s + v1;
             s = s + v2;
             s = s + v3;
-            dw[p0] = 0.0;
-            dw[p1] = 0.0;
-            dw[p2] = 0.0;
-            dw[p3] = 0.0;
+            if (zero) {
+                dw[p0] = 0.0;
+                dw[p1] = 0.0;
+                dw[p2] = 0.0;
+                dw[p3] = 0.0;
+            }
         }
         for (; q < e; ++q) {
             const uint32_t p = fpos[q];
             s = s + dw[p];
-            dw[p] = 0.0;
+            if (zero) dw[p] = 0.0;
         }
         if (apply)
             w[j] = w[j] + (s * mult);
@@ -141,10 +145,11 @@ __global__ __launch_bounds__(256) void fold_compact_kernel(double* dw, const int
 }
 
 void launch_fold_compact(double* dw, const int64_t* fptr, const uint32_t* fpos, int64_t d, double* dw_sum, double* w,
-                         double mult, bool apply, const int32_t* inv, hipStream_t s, const double* init) {
+                         double mult, bool apply, const int32_t* inv, bool zero, hipStream_t s, const double* init) {
     int blocks = (int)std::min<int64_t>((d + 255) / 256, 8192);
     if (blocks < 1) blocks = 1;
-    fold_compact_kernel<<<blocks, 256, 0, s>>>(dw, fptr, fpos, d, dw_sum, w, mult, apply ? 1 : 0, inv, init);
+    fold_compact_kernel<<<blocks, 256, 0, s>>>(dw, fptr, fpos, d, dw_sum, w, mult, apply ? 1 : 0, inv, init,
+                                               zero ? 1 : 0);
 }
 
 // Background re-zeroing of a folded deltaW set (double-buffered slices): a
