@@ -26,7 +26,7 @@ OBJS := $(BUILD)/kernels_strict.strict.o $(BUILD)/kernels_fast.fast.o $(BUILD)/e
         $(BUILD)/comm.o $(BUILD)/ingest.strict.o
 
 $(OUT): $(OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lpthread -ldl
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@.tmp $(OBJS) -lpthread -ldl && mv -f $@.tmp $@
 
 cocoa_amd/cocoa_driver: $(CSRC)/driver_main.cpp $(CSRC)/jdouble.h $(OUT) include/cocoa_capi.h
 	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude -I$(CSRC) -x c++ $< -o $@ -Lcocoa_amd -lcocoa_hip -Wl,-rpath,'$$ORIGIN'
@@ -62,8 +62,8 @@ variant:
 ubench: tools/ubench/calib tools/ubench/lat tools/ubench/ldsdma tools/ubench/dma_layout tools/ubench/evalspmv
 # eval-pass variants on the C2 shape (links the library for the generator and the shipped eval)
 tools/ubench/evalspmv: tools/ubench/evalspmv.hip $(CSRC)/eval_wave.h $(OUT)
-	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=fast -Iinclude -I$(CSRC) $< -o $@ -Lcocoa_amd -lcocoa_hip \
-	    -Wl,-rpath,'$$ORIGIN/../../cocoa_amd'
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=fast -Iinclude -I$(CSRC) $< -o $@.tmp -Lcocoa_amd -lcocoa_hip \
+	    -Wl,-rpath,'$$ORIGIN/../../cocoa_amd' && mv -f $@.tmp $@
 tools/ubench/%: tools/ubench/%.hip
 	$(HIPCC) -O2 --offload-arch=$(ARCH) $< -o $@
 

@@ -170,7 +170,10 @@ def main():
 
     def steps(t, count, stop=None):
         """count rounds from t, each evaluated; returns (values, rounds, t_next).
-        stop(value) -> True ends the loop at the first round whose value satisfies it."""
+        stop(value) -> True ends the loop at the first round whose value satisfies it.
+        In line (default): round t's evaluation is enqueued behind it
+        (cocoa_eval_begin) and read back (cocoa_eval_end) once round t+1 is
+        queued too, so the GPU does not wait on the host between rounds."""
         vals, rounds, pending = [], [], None
         for _ in range(count):
             runner.round(t)
@@ -183,13 +186,17 @@ def main():
                 eng.eval_async()
                 pending = t
             else:
-                vals.append(runner.eval()[key])
-                rounds.append(t)
-                if stop and stop(vals[-1]):
-                    return vals, rounds, t + 1
+                if pending is not None:
+                    vals.append(runner.eval_end()[key])
+                    rounds.append(pending)
+                    pending = None
+                    if stop and stop(vals[-1]):  # (round t is queued behind it; not evaluated)
+                        return vals, rounds, t + 1
+                runner.eval_begin()
+                pending = t
             t += 1
         if pending is not None:
-            vals.append(eng.eval_wait()[key])
+            vals.append(eng.eval_wait()[key] if pipe else runner.eval_end()[key])
             rounds.append(pending)
         return vals, rounds, t
 
@@ -205,6 +212,7 @@ def main():
     stats = eng.kernel_stats()
     # the eval pass alone (in the timed loop it overlaps the next round's solver)
     eng.stats_reset()
+    eng.sync()
     for _ in range(5):
         runner.eval()
     eval_alone = eng.kernel_stats().get("eval", {})

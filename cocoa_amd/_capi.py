@@ -103,6 +103,8 @@ SIGNATURES = {
     "cocoa_eval": (_int, [_vp, ctypes.POINTER(EvalResult)]),
     "cocoa_eval_async": (_int, [_vp]),
     "cocoa_eval_wait": (_int, [_vp, ctypes.POINTER(EvalResult)]),
+    "cocoa_eval_begin": (_int, [_vp]),
+    "cocoa_eval_end": (_int, [_vp, ctypes.POINTER(EvalResult)]),
     "cocoa_eval_finish": (_int, [_vp, _f64, _f64, _f64, _i64, _i64, ctypes.POINTER(EvalResult)]),
     "cocoa_run": (_int, [_vp, ctypes.POINTER(Params), ctypes.POINTER(Debug), _int, _pf64, ROUND_CB, _vp]),
     "cocoa_get_w": (_int, [_vp, _pf64]),

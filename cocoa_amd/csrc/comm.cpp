@@ -45,6 +45,10 @@ struct Rccl {
     ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*bcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     const char* (*err_str)(ncclResult_t) = nullptr;
+    // one process over several devices (GroupComm)
+    ncclResult_t (*init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
 };
 
 Rccl& rccl() {
@@ -63,6 +67,9 @@ Rccl& rccl() {
         r.recv = (decltype(r.recv))dlsym(r.so, "ncclRecv");
         r.bcast = (decltype(r.bcast))dlsym(r.so, "ncclBroadcast");
         r.err_str = (decltype(r.err_str))dlsym(r.so, "ncclGetErrorString");
+        r.init_all = (decltype(r.init_all))dlsym(r.so, "ncclCommInitAll");
+        r.group_start = (decltype(r.group_start))dlsym(r.so, "ncclGroupStart");
+        r.group_end = (decltype(r.group_end))dlsym(r.so, "ncclGroupEnd");
     });
     if (!r.so || !r.get_unique_id || !r.init_rank || !r.all_reduce || !r.send || !r.recv || !r.bcast)
         throw Error(COCOA_E_NODEV, "RCCL (librccl.so) is not available");
@@ -432,6 +439,35 @@ void Comm::bcast_last(double* buf, int64_t n, bool device, hipStream_t s) {
         HIPCHK_C(hipMemcpyAsync(buf, h, bytes, hipMemcpyHostToDevice, s));
         HIPCHK_C(hipStreamSynchronize(s));
     }
+}
+
+// ---- one process, several devices -------------------------------------------
+GroupComm* group_comm_create(const std::vector<int>& devices) {
+    Rccl& r = rccl();
+    if (!r.init_all || !r.group_start || !r.group_end || !r.destroy)
+        throw Error(COCOA_E_NODEV, "RCCL (librccl.so) has no ncclCommInitAll / ncclGroupStart");
+    GroupComm* g = new GroupComm();
+    g->comms.assign(devices.size(), nullptr);
+    const ncclResult_t rc = r.init_all((ncclComm_t*)g->comms.data(), (int)devices.size(), devices.data());
+    if (rc != ncclSuccess) {
+        delete g;
+        nccl_check(rc, "ncclCommInitAll");
+    }
+    return g;
+}
+
+GroupComm::~GroupComm() {
+    for (void* c : comms)
+        if (c && rccl().destroy) (void)rccl().destroy((ncclComm_t)c);
+}
+
+void GroupComm::allreduce(const std::vector<double*>& bufs, int64_t n, const std::vector<hipStream_t>& streams) {
+    Rccl& r = rccl();
+    nccl_check(r.group_start(), "ncclGroupStart");
+    for (size_t i = 0; i < comms.size(); ++i)
+        nccl_check(r.all_reduce(bufs[i], bufs[i], (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)comms[i], streams[i]),
+                   "ncclAllReduce");
+    nccl_check(r.group_end(), "ncclGroupEnd");
 }
 
 }  // namespace cocoa

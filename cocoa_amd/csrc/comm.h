@@ -58,6 +58,18 @@ struct Comm {
     double* scratch(int64_t n);
 };
 
+// One process driving several distinct devices (cocoa_create_multi): one RCCL
+// communicator per device from ncclCommInitAll, and the per-round deltaW sum
+// as one ncclAllReduce per device inside ncclGroupStart / ncclGroupEnd, each
+// on its device's stream behind that device's fold.  RCCL reduce-scatters then
+// all-gathers, so every device holds the same bytes.
+struct GroupComm {
+    std::vector<void*> comms;  // ncclComm_t per device, in member order
+    ~GroupComm();
+    void allreduce(const std::vector<double*>& bufs, int64_t n, const std::vector<hipStream_t>& streams);
+};
+GroupComm* group_comm_create(const std::vector<int>& devices);
+
 // uid for `transport` (128 bytes); HOST opens the listening socket in this
 // process, so rank 0 must create it.
 void comm_unique_id(int transport, void* uid);

@@ -146,6 +146,10 @@ struct cocoa_ctx {
     // as a member of a multi-device context (fast mode): slice r of the other
     // members' folds, gathered for this member's part of the reduce-scatter
     DevBuf x_stage;
+    // fast exchange over distinct devices: RCCL (one communicator per device,
+    // grouped all-reduce); null: the peer-copy reduce-scatter / all-gather
+    cocoa::GroupComm* g_rccl = nullptr;
+    std::string g_exchange;  // "rccl", "peer" or "chain" (strict), for cocoa_plan_info
     bool is_group() const { return !subs.empty(); }
     // rank exchange (cocoa_comm_init): owned; null = single rank / caller-driven
     cocoa::Comm* comm = nullptr;
@@ -182,6 +186,12 @@ struct cocoa_ctx {
     bool compact_ready = false, dw_compact = false;
     int64_t max_u = 0, sum_u = 0;
     DevBuf col_local, fptr, fpos;
+    // fast mode: the column-block fold of compact slices (fold_blocks_kernel):
+    // per slice position its column's offset in its kFoldJ-column block, per
+    // (block, partition) the slice's first position in the block, the work
+    // items (block, partition range) and the device-order accumulator
+    DevBuf fcol16, fbnd, fitems, ftmp;
+    int32_t n_fitems = 0, n_fblk = 0;
     int32_t max_nl = 0, min_nl = 0;
     // test data (this rank)
     Csr te;
@@ -246,6 +256,12 @@ struct cocoa_ctx {
     hipStream_t estream = nullptr;
     hipEvent_t e_round = nullptr, e_done = nullptr;
     bool eval_pending = false;  // snapshots taken (cocoa_eval_async), result not yet collected
+    // cocoa_eval_begin: an in-line evaluation enqueued, its sums read back by
+    // cocoa_eval_end (single rank, one device); other contexts hold the finished
+    // result in eval_held
+    bool inl_pending = false;
+    hipEvent_t e_inl = nullptr;
+    cocoa_eval_result eval_held{};
     bool eval_fired = false;    //   and its kernels enqueued on estream
     DevBuf w_snap, alpha_snap, eval_part2, eval_out2;
     void eval_quiesce();        // the pending evaluation (if any) runs to completion and is dropped
@@ -309,6 +325,14 @@ struct cocoa_ctx {
         pending.clear();
     }
     ~cocoa_ctx() {
+        if (g_rccl) {
+            for (cocoa_ctx* sub : subs) {
+                (void)hipSetDevice(sub->device);
+                if (sub->stream) (void)hipStreamSynchronize(sub->stream);
+            }
+            delete g_rccl;
+            g_rccl = nullptr;
+        }
         for (size_t r = 0; r < subs.size(); ++r) {
             (void)hipSetDevice(subs[r]->device);
             if (r < g_ev.size() && g_ev[r]) (void)hipEventDestroy(g_ev[r]);
@@ -329,6 +353,9 @@ struct cocoa_ctx {
             (void)hipStreamDestroy(estream);
             (void)hipEventDestroy(e_round);
             (void)hipEventDestroy(e_done);
+        }
+        if (e_inl) {
+            (void)hipEventDestroy(e_inl);
         }
         delete comm;
         if (zstream) {
@@ -581,6 +608,51 @@ static void build_compact(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* p
     upload_padded(c->col_local, cl.data(), sizeof(int32_t) * (size_t)nnz, s);
     upload(c->fptr, fp.data(), sizeof(int64_t) * fp.size(), s);
     upload(c->fpos, pos.data(), sizeof(uint32_t) * pos.size(), s);
+    c->fcol16.free();
+    c->fbnd.free();
+    c->fitems.free();
+    c->ftmp.free();
+    c->n_fitems = c->n_fblk = 0;
+    if (!c->strict) {
+        // Fast fold by column blocks (fold_blocks_kernel): block b = device
+        // columns [b J, (b+1) J); each slice lists its columns in device order,
+        // so block b's entries of slice k are the contiguous positions
+        // [fbnd[b][k], fbnd[b+1][k]).  Work items cut each block's partition
+        // range into pieces of about kFoldItem entries.
+        const int64_t J = kFoldJ, nblk = (d + J - 1) / J;
+        std::vector<uint32_t> bnd((size_t)(nblk + 1) * (size_t)K);
+        std::vector<uint16_t> fc((size_t)K * (size_t)mu, 0);
+        for (int k = 0; k < K; ++k) {
+            const std::vector<int32_t>& L = lists[(size_t)k];
+            size_t i = 0;
+            for (int64_t b = 0; b <= nblk; ++b) {
+                while (i < L.size() && L[i] < b * J) ++i;
+                bnd[(size_t)b * K + k] = (uint32_t)i;
+            }
+            for (size_t q = 0; q < L.size(); ++q) fc[(size_t)k * mu + q] = (uint16_t)(L[q] & (J - 1));
+        }
+        std::vector<int32_t> items;  // (block, k0, k1, sole)
+        for (int64_t b = 0; b < nblk; ++b) {
+            int64_t acc = 0;
+            int k0 = 0;
+            const size_t first = items.size();
+            for (int k = 0; k < K; ++k) {
+                acc += bnd[(size_t)(b + 1) * K + k] - bnd[(size_t)b * K + k];
+                if (acc >= kFoldItem || k == K - 1) {
+                    items.insert(items.end(), {(int32_t)b, k0, k + 1, 0});
+                    k0 = k + 1;
+                    acc = 0;
+                }
+            }
+            if (items.size() - first == 4) items[first + 3] = 1;  // the block's only item: plain stores
+        }
+        upload(c->fbnd, bnd.data(), sizeof(uint32_t) * bnd.size(), s);
+        upload_padded(c->fcol16, fc.data(), sizeof(uint16_t) * fc.size(), s);
+        upload(c->fitems, items.data(), sizeof(int32_t) * items.size(), s);
+        c->ftmp.alloc_zero(sizeof(double) * (size_t)d, s);
+        c->n_fitems = (int32_t)(items.size() / 4);
+        c->n_fblk = (int32_t)nblk;
+    }
     HIPCHK(hipStreamSynchronize(s));
     c->max_u = mu;
     c->sum_u = su;
@@ -867,19 +939,37 @@ static int solver_mode(int m) {
 static int32_t wrap32(int64_t x) { return (int32_t)(uint32_t)(uint64_t)x; }
 
 // vec_len: length of the solver's mutable vector (d, or the compact slice)
-static void plan_solver(cocoa_ctx* c, int64_t vec_len) {
+// LDS layout of the chain solver (one workgroup per partition).  need_prod:
+// the loader forms x.w itself (no step plan: the unit API), which needs the
+// product buffer.  With more partitions than CUs (C4 on one GPU: 1,024 on
+// 256) the workgroups queue for CUs, so the layout is sized for
+// ceil(K_loc / CUs) workgroups per CU (at most 4): the stream buffers shrink
+// (1,024 or 512 staged entries per batch instead of 2,048) and alpha moves to
+// HBM when it does not fit.  (r03: 93.5 KB, one workgroup per CU, the 1,024
+// C4 chains ran four after another.)
+static void plan_solver(cocoa_ctx* c, int64_t vec_len, bool need_prod = true) {
     SolverArgs& a = c->sa;
     size_t off = 0;
     const size_t vec_bytes = align16(sizeof(double) * (size_t)vec_len);
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int want = (int)std::min<int64_t>(4, std::max<int64_t>(1, ((int64_t)c->K_loc + ncu - 1) / std::max(ncu, 1)));
+    const size_t budget = want > 1 ? (kLdsMax / (size_t)want) & ~(size_t)1023 : kLdsMax;
     // long rows (dense data, C3: 2,000 entries) would leave one row per batch and
     // make the loader's per-batch latency the bound: double the stream instead
     // (alpha then moves to HBM when it no longer fits; the chain prefetches it)
     const double zavg = c->tr.n ? (double)c->tr.nnz / (double)c->tr.n : 0.0;
-    const size_t cap = zavg * 4 > (double)kStreamCap ? 2 * (size_t)kStreamCap : (size_t)kStreamCap;
-    const size_t fixed = 2 * align16(cap * 4) + 2 * align16(cap * 8) + 2 * align16(sizeof(BatchMeta)) +
-                         align16(cap * 8) + align16(sizeof(double) * kRegChunks * 64);
-    size_t avail = kLdsMax - fixed;
-    c->vec_lds = is_sdca(c->method) && vec_bytes <= avail;
+    size_t cap = zavg * 4 > (double)kStreamCap ? 2 * (size_t)kStreamCap : (size_t)kStreamCap;
+    auto fixed_for = [&](size_t cp) {
+        return 2 * align16(cp * 4) + 2 * align16(cp * 8) + 2 * align16(sizeof(BatchMeta)) +
+               (need_prod ? align16(cp * 8) : 0) + align16(sizeof(double) * kRegChunks * 64);
+    };
+    // several workgroups per CU: no LDS-resident vector, stream of at least 512
+    // entries (a batch still holds a few rows)
+    while (want > 1 && cap > 512 && fixed_for(cap) > budget) cap /= 2;
+    const size_t fixed = fixed_for(cap);
+    size_t avail = (want > 1 ? budget : kLdsMax) - std::min(fixed, budget);
+    c->vec_lds = is_sdca(c->method) && vec_bytes <= avail && want == 1;
     if (c->vec_lds) avail -= vec_bytes;
     const size_t al_bytes = align16(sizeof(double) * (size_t)std::max(c->max_nl, 1));
     c->alpha_lds = is_sdca(c->method) && al_bytes <= avail;
@@ -895,8 +985,8 @@ static void plan_solver(cocoa_ctx* c, int64_t vec_len) {
         a.lds_meta[b] = (int32_t)off;
         off += align16(sizeof(BatchMeta));
     }
-    a.lds_prod = (int32_t)off;
-    off += align16(cap * 8);
+    a.lds_prod = (int32_t)off;  // (aliases the scratch when unused: never touched then)
+    if (need_prod) off += align16(cap * 8);
     a.lds_scratch = (int32_t)off;
     off += align16(sizeof(double) * kRegChunks * 64);
     if (c->alpha_lds) {
@@ -1011,7 +1101,9 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     }
     const bool need_wloc = method == COCOA_METHOD_COCOA || method == COCOA_METHOD_LOCALSGD;
     ctx->method = method;
-    plan_solver(ctx, slice);
+    // every SDCA round runs the step plan (use_plan below), so the chain
+    // solver's loader never forms x.w itself: no product buffer
+    plan_solver(ctx, slice, !is_sdca(method));
     if (need_wloc && !(method == COCOA_METHOD_COCOA && ctx->vec_lds))
         ctx->wloc.alloc(sizeof(double) * (size_t)(K * d));
     else
@@ -1373,7 +1465,11 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             c->comm->chain_recv(c->dw_sum, d, true, s);
     }
     c->timed(COCOA_K_FOLD, [&] {
-        if (c->dw_compact)
+        if (c->dw_compact && c->n_fitems > 0 && c->dw_dbuf && !chain_init)
+            launch_fold_blocks(dws, c->fcol16.as<uint16_t>(), c->fbnd.as<uint32_t>(), c->fitems.as<int32_t>(),
+                               c->n_fitems, K, c->max_u, d, c->ftmp.as<double>(), c->dw_sum, c->w.as<double>(),
+                               c->mult, fuse_apply, c->d_inv.as<int32_t>(), s);
+        else if (c->dw_compact)
             launch_fold_compact(dws, c->fptr.as<int64_t>(), c->fpos.as<uint32_t>(), d, c->dw_sum, c->w.as<double>(),
                                 c->mult, fuse_apply, c->d_inv.as<int32_t>(), !c->dw_dbuf, s, chain_init);
         else
@@ -1675,6 +1771,7 @@ static void group_eval(cocoa_ctx* g, cocoa_eval_result* out);
 extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     CAPI_BEGIN(ctx)
     require(out != nullptr, COCOA_E_ARG, "null out");
+    require(!ctx->inl_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_end first");
     if (ctx->is_group()) {
         group_eval(ctx, out);
         return COCOA_OK;
@@ -1715,6 +1812,7 @@ extern "C" int cocoa_eval_async(cocoa_ctx* ctx) {
             "cocoa_eval_async: fast mode on a single rank only (use cocoa_eval)");
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     require(!ctx->eval_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_wait first");
+    require(!ctx->inl_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_end first");
     if (!ctx->estream) {
         HIPCHK(hipStreamCreateWithFlags(&ctx->estream, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&ctx->e_round, hipEventDisableTiming));
@@ -1747,6 +1845,10 @@ static void eval_fire(cocoa_ctx* ctx) {
 }
 
 void cocoa_ctx::eval_quiesce() {
+    if (inl_pending) {  // an uncollected cocoa_eval_begin: its result is dropped
+        HIPCHK(hipEventSynchronize(e_inl));
+        inl_pending = false;
+    }
     if (!eval_pending) return;
     eval_fire(this);
     HIPCHK(hipEventSynchronize(e_done));
@@ -1765,6 +1867,49 @@ extern "C" int cocoa_eval_wait(cocoa_ctx* ctx, cocoa_eval_result* out) {
     // evaluation fired) may still run on ctx->stream, so its status word is
     // read by the next call that synchronises that stream (cocoa_sync / cocoa_eval)
     const double* h = ctx->h_eval + 4;
+    finish(ctx, h[0], h[1], h[2], (int64_t)h[3], (int64_t)(ctx->has_test ? ctx->te.n : 0), out);
+    CAPI_END(ctx)
+}
+
+// In-line evaluation with deferred read-back: the same pass as cocoa_eval,
+// enqueued on the context's stream (so the next round's plan still reuses its
+// row x.w), its sums copied to pinned memory behind it; the caller enqueues
+// the next round before collecting them, and the GPU never idles while the
+// host reads a round's gap.  Multi-rank and multi-device contexts evaluate at
+// once (their merges exchange in order) and hand the result over at
+// cocoa_eval_end.
+extern "C" int cocoa_eval_begin(cocoa_ctx* ctx) {
+    CAPI_BEGIN(ctx)
+    require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
+    require(!ctx->inl_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_end first");
+    require(!ctx->eval_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_wait first");
+    if (ctx->is_group() || (ctx->comm && ctx->comm->world > 1)) {
+        cocoa_eval_result r{};
+        const int rc = cocoa_eval(ctx, &r);
+        if (rc != COCOA_OK) return rc;
+        ctx->eval_held = r;
+    } else {
+        if (!ctx->e_inl) HIPCHK(hipEventCreateWithFlags(&ctx->e_inl, hipEventDisableTiming));
+        eval_launch(ctx);
+        HIPCHK(hipEventRecord(ctx->e_inl, ctx->stream));
+    }
+    ctx->inl_pending = true;
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_eval_end(cocoa_ctx* ctx, cocoa_eval_result* out) {
+    CAPI_BEGIN(ctx)
+    require(out != nullptr, COCOA_E_ARG, "null out");
+    require(ctx->inl_pending, COCOA_E_STATE, "cocoa_eval_end: no evaluation pending (cocoa_eval_begin)");
+    ctx->inl_pending = false;
+    if (ctx->is_group() || (ctx->comm && ctx->comm->world > 1)) {
+        *out = ctx->eval_held;
+        return COCOA_OK;
+    }
+    HIPCHK(hipEventSynchronize(ctx->e_inl));
+    // (no check_status: a round enqueued since may still run; the next
+    // synchronising call reads the solver's status word)
+    const double* h = ctx->h_eval;
     finish(ctx, h[0], h[1], h[2], (int64_t)h[3], (int64_t)(ctx->has_test ? ctx->te.n : 0), out);
     CAPI_END(ctx)
 }
@@ -2161,7 +2306,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     if (!plus) ctx->to_host_order(wdev, w);
     if (delta_alpha)
         for (int32_t i = 0; i < nl; ++i) delta_alpha[i] = alpha[i] - old[(size_t)i];  // CoCoA.scala:190
-    if (ctx->inited) plan_solver(ctx, ctx->dw_compact ? ctx->max_u : d);
+    if (ctx->inited) plan_solver(ctx, ctx->dw_compact ? ctx->max_u : d, !is_sdca(ctx->method));
     CAPI_END(ctx)
 }
 
@@ -2258,6 +2403,26 @@ extern "C" int cocoa_create_multi(int32_t n_devices, const int32_t* devices, int
                 }
             }
         HIPCHK(hipSetDevice(g->device));
+        // fast mode over distinct devices: the deltaW sum as RCCL all-reduces
+        // (COCOA_GROUP_EXCHANGE=peer keeps the peer-copy reduce-scatter); any
+        // RCCL failure at set-up falls back to the peer copies
+        g->g_exchange = g->strict ? "chain" : "peer";
+        bool distinct = n_devices > 1 && !g->strict;
+        for (int32_t a = 0; a < n_devices && distinct; ++a)
+            for (int32_t b = a + 1; b < n_devices; ++b)
+                if (g->subs[(size_t)a]->device == g->subs[(size_t)b]->device) distinct = false;
+        const char* ge = std::getenv("COCOA_GROUP_EXCHANGE");
+        if (distinct && !(ge && std::strcmp(ge, "peer") == 0)) {
+            std::vector<int> devs;
+            for (cocoa_ctx* sub : g->subs) devs.push_back(sub->device);
+            try {
+                g->g_rccl = cocoa::group_comm_create(devs);
+                g->g_exchange = "rccl";
+            } catch (const Error&) {
+                g->g_rccl = nullptr;
+            }
+            HIPCHK(hipSetDevice(g->device));
+        }
     } catch (const Error& e) {
         cocoa_set_global_error(e.what());
         delete g;
@@ -2423,6 +2588,30 @@ static void group_round(cocoa_ctx* g, int32_t t) {
             HIPCHK(hipEventRecord(g->g_ev[r], sub->stream));
         }
         owner = N - 1;
+    } else if (g->g_rccl) {
+        // distinct devices: every member folds its partitions, then one grouped
+        // RCCL all-reduce of the folds (each on its member's stream, behind the
+        // fold), then the identical w update on every member
+        std::vector<double*> bufs;
+        std::vector<hipStream_t> streams;
+        for (size_t r = 0; r < N; ++r) {
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipSetDevice(sub->device));
+            run_local(sub, t, false);
+            bufs.push_back(sub->dw_sum);
+            streams.push_back(sub->stream);
+        }
+        g->g_rccl->allreduce(bufs, g->d, streams);
+        for (size_t r = 0; r < N; ++r) {
+            cocoa_ctx* sub = g->subs[r];
+            HIPCHK(hipSetDevice(sub->device));
+            sub->timed(COCOA_K_APPLY, [&] {
+                launch_apply(sub->w.as<double>(), sub->dw_sum, sub->d, sub->mult, sub->d_inv.as<int32_t>(), sub->stream);
+            });
+            sub->xw_cached = false;
+        }
+        HIPCHK(hipSetDevice(g->device));
+        return;
     } else {
         // Every member folds its partitions; then a reduce-scatter and an
         // all-gather of column slices, all on the members' own streams: member
@@ -2625,7 +2814,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
         sub_check(cocoa_plan_info(ctx->subs[0], buf, len), ctx->subs[0]);
         std::string p(buf);
         if (!p.empty() && p.back() == '}') p.pop_back();
-        p += ",\"n_devices\":" + std::to_string(ctx->subs.size()) + "}";
+        p += ",\"n_devices\":" + std::to_string(ctx->subs.size()) + ",\"exchange\":\"" + ctx->g_exchange + "\"}";
         require((int)p.size() < len, COCOA_E_ARG, "cocoa_plan_info: buffer too small");
         std::memcpy(buf, p.c_str(), p.size() + 1);
         return COCOA_OK;
@@ -2634,11 +2823,12 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
-                  "\"sum_u\":%lld}",
+                  "\"sum_u\":%lld,\"fold\":\"%s\"}",
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,
                   ctx->dw_dbuf ? 1 : 0, ctx->use_dense ? "dense" : ctx->use_gram ? "gram" : "chain",
-                  ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u);
+                  ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u,
+                  !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather");
     CAPI_END(ctx)
 }

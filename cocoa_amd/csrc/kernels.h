@@ -251,6 +251,14 @@ void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double*
                  const int32_t* inv, bool zero, hipStream_t s, const double* init = nullptr);
 // compact deltaW slices: column j's sum is the gather of dw[fpos[fptr[j] ..
 // fptr[j+1])] in partition order (each entry re-zeroed as it is read)
+// fast mode, compact slices: the fold by column blocks of kFoldJ device
+// columns (LDS accumulators, work items of ~kFoldItem entries); reads only
+// (the double-buffered set is re-zeroed by a memset)
+constexpr int64_t kFoldJ = 4096;
+constexpr int64_t kFoldItem = 32768;
+void launch_fold_blocks(const double* dw, const uint16_t* fcol16, const uint32_t* fbnd, const int32_t* items,
+                        int32_t n_items, int32_t K, int64_t max_u, int64_t d, double* tmp, double* dw_sum, double* w,
+                        double mult, bool apply, const int32_t* inv, hipStream_t s);
 void launch_fold_compact(double* dw, const int64_t* fptr, const uint32_t* fpos, int64_t d, double* dw_sum, double* w,
                          double mult, bool apply, const int32_t* inv, bool zero, hipStream_t s,
                          const double* init = nullptr);

@@ -262,6 +262,7 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     }
 }
 
+#ifdef COCOA_DIAG
 // Row-parallel variant: one 16-lane group per row, straight from global memory
 // (no LDS staging, no barriers), U loads per lane in flight per row chunk,
 // rows walked grid-stride so every wave always has rows of its own in flight.
@@ -326,6 +327,8 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(EvalArgs a) {
     }
 }
 
+#endif
+
 __global__ __launch_bounds__(256) void eval_final_kernel(const double* partials, int blocks, double* out) {
     __shared__ double red[4][4];
     const int tid = threadIdx.x;
@@ -348,17 +351,9 @@ int eval_fast_blocks(int64_t n_tiles, int64_t n_t_tiles) {
     return (int)(b < 1 ? 1 : b);
 }
 
-static int eval_variant();
-int eval_tile_entries() {
 #ifdef COCOA_DIAG
-    // diagnostic builds only (make diag): A/B of the tile size
-    if (const char* e = getenv("COCOA_EVAL_TILE")) return atoi(e) == 2048 ? 2048 : kEvalTile;
-#endif
-    return (eval_variant() >= 6 && eval_variant() <= 9) ? 2048 : kEvalTile;
-}
-
-// eval variant (A/B while measuring): 0 = row tiles through LDS, 1 = rows
-// from global with 8 loads per lane in flight, 2 = 4 loads
+// diagnostic builds only (make diag): A/B variants of the pass (DESIGN.md
+// section 3.3 lists what each measured; results of 3 and 4 are invalid)
 static int eval_variant() {
     static int v = -1;
     if (v < 0) {
@@ -367,12 +362,16 @@ static int eval_variant() {
     }
     return v;
 }
+int eval_tile_entries() {
+    if (const char* e = getenv("COCOA_EVAL_TILE")) return atoi(e) == 2048 ? 2048 : kEvalTile;
+    return (eval_variant() >= 6 && eval_variant() <= 9) ? 2048 : kEvalTile;
+}
 
-void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
-    const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
-    if (eval_variant() == 8 || eval_variant() == 9) {  // 2,048-entry tiles, more blocks per CU
+static bool launch_eval_diag(const EvalArgs& a, bool c16, hipStream_t s) {
+    const int v = eval_variant();
+    if (v == 8 || v == 9) {  // 2,048-entry tiles, more blocks per CU
         const int64_t nt = a.n_tiles + a.n_t_tiles;
-        if (eval_variant() == 8) {  // 512 threads, 4 blocks per CU
+        if (v == 8) {  // 512 threads, 4 blocks per CU
             const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(nt, 1024));
             if (c16) eval_stream_kernel<2048, 512, true><<<nb, 512, 0, s>>>(a);
             else eval_stream_kernel<2048, 512, false><<<nb, 512, 0, s>>>(a);
@@ -383,15 +382,15 @@ void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
             else eval_stream_kernel<2048, 256, false><<<nb, 256, 0, s>>>(a);
             eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
         }
-        return;
+        return true;
     }
-    if (eval_variant() >= 5) {  // hot w columns in LDS
+    if (v >= 5 && c16) {  // hot w columns in LDS (uint16 columns only)
         const int nb = eval_fast_blocks(a.n_tiles, a.n_t_tiles);
-        if (eval_variant() == 5) {  // 4,096-entry tiles, 32 KB of w: 2 blocks per CU
+        if (v == 5) {  // 4,096-entry tiles, 32 KB of w: 2 blocks per CU
             const int n2 = (int)std::min<int64_t>(a.n_tiles + a.n_t_tiles, 512);
             eval_stream_kernel<kEvalTile, 512, true, 0, 4096><<<n2, 512, 0, s>>>(a);
             eval_final_kernel<<<1, 256, 0, s>>>(a.partials, n2, a.out);
-        } else if (eval_variant() == 6) {  // 2,048-entry tiles, 32 KB of w: 3 blocks per CU
+        } else if (v == 6) {  // 2,048-entry tiles, 32 KB of w: 3 blocks per CU
             eval_stream_kernel<2048, 512, true, 0, 4096><<<nb, 512, 0, s>>>(a);
             eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
         } else {  // 2,048-entry tiles, 64 KB of w (8,192 columns): 2 blocks per CU
@@ -399,18 +398,18 @@ void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
             eval_stream_kernel<2048, 512, true, 0, 8192><<<n2, 512, 0, s>>>(a);
             eval_final_kernel<<<1, 256, 0, s>>>(a.partials, n2, a.out);
         }
-        return;
+        return true;
     }
-    if (eval_variant() >= 3) {  // timing diagnostics (results invalid)
+    if ((v == 3 || v == 4) && c16) {  // timing diagnostics (results invalid)
         const int nb = eval_fast_blocks(a.n_tiles, a.n_t_tiles);
-        if (eval_variant() == 3) eval_stream_kernel<kEvalTile, 512, true, 1><<<nb, 512, 0, s>>>(a);
+        if (v == 3) eval_stream_kernel<kEvalTile, 512, true, 1><<<nb, 512, 0, s>>>(a);
         else eval_stream_kernel<kEvalTile, 512, true, 2><<<nb, 512, 0, s>>>(a);
         eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
-        return;
+        return true;
     }
-    if (eval_variant() != 0) {
-        const int nb = 2048;  // 8 blocks of 256 threads per CU, persistent
-        if (eval_variant() == 1) {
+    if (v == 1 || v == 2) {  // one 16-lane group per row, 8 / 4 loads per lane in flight
+        const int nb = 2048;
+        if (v == 1) {
             if (c16) eval_rows_kernel<8, true><<<nb, 256, 0, s>>>(a);
             else eval_rows_kernel<8, false><<<nb, 256, 0, s>>>(a);
         } else {
@@ -418,16 +417,123 @@ void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
             else eval_rows_kernel<4, false><<<nb, 256, 0, s>>>(a);
         }
         eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
-        return;
+        return true;
     }
-    if (eval_tile_entries() == 2048) {
-        if (c16) eval_stream_kernel<2048, 512, true><<<blocks, 512, 0, s>>>(a);
-        else eval_stream_kernel<2048, 512, false><<<blocks, 512, 0, s>>>(a);
-    } else if (c16)
+    return false;
+}
+#else
+int eval_tile_entries() { return kEvalTile; }
+#endif
+
+void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
+    const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
+#ifdef COCOA_DIAG
+    if (launch_eval_diag(a, c16, s)) return;
+#endif
+    if (c16)
         eval_stream_kernel<kEvalTile, 512, true><<<blocks, 512, 0, s>>>(a);
     else
         eval_stream_kernel<kEvalTile, 512, false><<<blocks, 512, 0, s>>>(a);
     eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+}
+
+// --------------------------------------------- compact fold by blocks --
+// Fast-mode fold of compact deltaW slices (C4: 1,024 slices of up to 64,847
+// positions, 62 M live entries).  The per-column gather fold
+// (fold_compact_kernel) reads slice k at position i_k(j) for column j: for a
+// column held by a few hundred partitions the lanes of a wave land in
+// different slices, so almost every 8-byte read costs a whole line (1.65 ms
+// per C4 round, r03).  Here a work item takes one block of kFoldJ device
+// columns over a range of partitions: since every slice lists its columns in
+// device order, the block's entries of slice k are the contiguous run
+// [fbnd[b][k], fbnd[b+1][k]), read with consecutive lanes and added into an
+// LDS accumulator of the block's columns.  The block takes 64 partitions at a
+// time: lane l holds run l's bounds, a prefix sum packs the 64 runs, and each
+// lane finds the run of its packed position by a 6-step search over the
+// lanes, so short runs (the cold blocks: a few entries per slice) cost no
+// per-partition loop, and long ones (the hot blocks: thousands per slice) are
+// shared by all four waves, four 64-entry pieces per wave in flight.  The block's sums then go to tmp (a plain store when the
+// item is the block's only one, else an fp64 atomic add), and fold_finish
+// moves tmp into the rank's sum (original order) or into w, re-zeroing tmp.
+// Sums are reassociated and atomic: fast mode.
+__global__ __launch_bounds__(256) void fold_blocks_kernel(const double* dw, const uint16_t* fcol16,
+                                                          const uint32_t* fbnd, const int32_t* items, int32_t K,
+                                                          int64_t max_u, int64_t d, double* tmp) {
+    constexpr int kUn = 4;  // 64-entry pieces per wave in flight
+    __shared__ double acc[kFoldJ];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int32_t* it = items + 4 * (size_t)blockIdx.x;
+    const int32_t b = it[0], k0 = it[1], k1 = it[2], sole = it[3];
+    for (int i = tid; i < kFoldJ; i += 256) acc[i] = 0.0;
+    __syncthreads();
+    // the whole block walks the partitions 64 at a time; the 4 waves share each
+    // group's packed entries, kUn pieces of 64 per wave in flight
+    for (int32_t kk = k0; kk < k1; kk += 64) {
+        const int32_t k = kk + lane;
+        const bool ok = k < k1;
+        const int32_t lo = ok ? (int32_t)fbnd[(size_t)b * K + k] : 0;
+        const int32_t n = ok ? (int32_t)fbnd[(size_t)(b + 1) * K + k] - lo : 0;
+        const int32_t incl = wave_incl_scan(n);
+        const int32_t T = __shfl(incl, 63, 64);
+        const int32_t excl = incl - n;
+        for (int32_t q0 = 64 * kUn * wv; q0 < T; q0 += 64 * kUn * 4) {
+            size_t pos[kUn];
+            bool val[kUn];
+#pragma unroll
+            for (int u = 0; u < kUn; ++u) {
+                const int32_t q = q0 + 64 * u + lane;
+                // largest lane j with excl_j <= q (every lane active in the shuffles)
+                int j = 0;
+#pragma unroll
+                for (int st = 32; st >= 1; st >>= 1) {
+                    const int32_t e = __shfl(excl, j + st, 64);
+                    if (e <= q) j += st;
+                }
+                const int32_t lj = __shfl(lo, j, 64), ej = __shfl(excl, j, 64);
+                val[u] = q < T;
+                pos[u] = val[u] ? (size_t)(kk + j) * (size_t)max_u + (size_t)(lj + (q - ej)) : 0;
+            }
+            uint16_t c[kUn];
+            double v[kUn];
+#pragma unroll
+            for (int u = 0; u < kUn; ++u) {
+                c[u] = fcol16[pos[u]];
+                v[u] = dw[pos[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < kUn; ++u)
+                if (val[u]) atomicAdd(&acc[c[u]], v[u]);
+        }
+    }
+    __syncthreads();
+    const int64_t j0 = (int64_t)b * kFoldJ;
+    for (int i = tid; i < kFoldJ && j0 + i < d; i += 256) {
+        const double x = acc[i];
+        if (sole)
+            tmp[j0 + i] = x;
+        else if (x != 0.0)
+            unsafeAtomicAdd(tmp + j0 + i, x);
+    }
+}
+
+__global__ __launch_bounds__(256) void fold_finish_kernel(double* tmp, int64_t d, double* dw_sum, double* w,
+                                                          double mult, int apply, const int32_t* inv) {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < d; j += (int64_t)gridDim.x * 256) {
+        const double v = tmp[j];
+        tmp[j] = 0.0;
+        if (apply)
+            w[j] = w[j] + v * mult;
+        else
+            dw_sum[inv ? inv[j] : j] = v;
+    }
+}
+
+void launch_fold_blocks(const double* dw, const uint16_t* fcol16, const uint32_t* fbnd, const int32_t* items,
+                        int32_t n_items, int32_t K, int64_t max_u, int64_t d, double* tmp, double* dw_sum, double* w,
+                        double mult, bool apply, const int32_t* inv, hipStream_t s) {
+    if (n_items > 0) fold_blocks_kernel<<<n_items, 256, 0, s>>>(dw, fcol16, fbnd, items, K, max_u, d, tmp);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((d + 255) / 256, 4096));
+    fold_finish_kernel<<<blocks, 256, 0, s>>>(tmp, d, dw_sum, w, mult, apply ? 1 : 0, inv);
 }
 
 // ------------------------------------------------------------ dense rows --

@@ -40,3 +40,9 @@ class DistributedCoCoA:
 
     def eval(self):
         return self.engine.eval()
+
+    def eval_begin(self):
+        self.engine.eval_begin()
+
+    def eval_end(self):
+        return self.engine.eval_end()

@@ -192,6 +192,16 @@ class Engine:
         C.check(C.lib().cocoa_eval_wait(self.h, ctypes.byref(r)), self.h)
         return r.as_dict()
 
+    def eval_begin(self):
+        """cocoa_eval_begin: the in-line evaluation of the current state, its
+        read-back deferred to eval_end (enqueue the next round in between)."""
+        C.check(C.lib().cocoa_eval_begin(self.h), self.h)
+
+    def eval_end(self):
+        r = C.EvalResult()
+        C.check(C.lib().cocoa_eval_end(self.h, ctypes.byref(r)), self.h)
+        return r.as_dict()
+
     def eval_finish(self, hinge_sum, alpha_sum, w_sq, err, test_rows):
         r = C.EvalResult()
         C.check(C.lib().cocoa_eval_finish(self.h, hinge_sum, alpha_sum, w_sq, int(err), int(test_rows),

@@ -228,6 +228,17 @@ int cocoa_eval(cocoa_ctx *ctx, cocoa_eval_result *out);
  * cocoa_eval refuses while one is. */
 int cocoa_eval_async(cocoa_ctx *ctx);
 int cocoa_eval_wait(cocoa_ctx *ctx, cocoa_eval_result *out);
+/* The cocoa_eval pass with deferred read-back: cocoa_eval_begin enqueues it
+ * on the context's stream behind the current round (the next round's step
+ * plan still reuses its per-row x.w) and returns at once; the caller enqueues
+ * the next cocoa_round and then collects with cocoa_eval_end, which returns
+ * exactly what cocoa_eval would have for that state.  The reference prints
+ * after round t before starting round t+1 (CoCoA.scala:51-56); here round t+1
+ * is already queued while the host reads round t's gap, so the GPU does not
+ * idle on the host.  Multi-rank and multi-device contexts evaluate inside
+ * cocoa_eval_begin.  One evaluation may be pending at a time. */
+int cocoa_eval_begin(cocoa_ctx *ctx);
+int cocoa_eval_end(cocoa_ctx *ctx, cocoa_eval_result *out);
 int cocoa_eval_finish(const cocoa_ctx *ctx, double hinge_sum, double alpha_sum, double w_sqnorm,
                       int64_t test_err_count, int64_t test_rows, cocoa_eval_result *out);
 

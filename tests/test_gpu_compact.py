@@ -86,7 +86,7 @@ def test_c4_share_uses_compact_slices():
     e.set_train(sh.train, part_begin=sh.part_begin, num_parts_global=sh.k_glob)
     e.init("cocoa+", sh.n_glob, 1, sh.H, sh.lam)
     p = e.plan()
-    assert p["dw_compact"] == 1 and p["dw_dbuf"] == 0 and p["solver"] == "gram"
+    assert p["dw_compact"] == 1 and p["dw_dbuf"] == 1 and p["solver"] == "gram" and p["fold"] == "blocks"
     assert p["max_u"] * 8 < sh.train.num_features
 
 
@@ -120,3 +120,23 @@ def test_compact_slices_fast_chain_vs_oracle(monkeypatch):
     wr = r.w()
     assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
     assert np.max(np.abs(e.alpha() - r.alpha())) <= REL
+
+
+@pytest.mark.parametrize("solver", ["gram", "chain"])
+def test_block_fold_matches_gather_fold(solver, monkeypatch):
+    """Fast mode folds compact slices by column blocks (double-buffered sets,
+    fold_blocks_kernel); a single slice set keeps the per-column gather fold
+    that zeroes as it reads.  Same rounds, same results within 1e-12 (the
+    block fold reassociates the partition sums)."""
+    sh = configs.share("c4", n=40000, d=400000, parts=32, n_test=2000)
+    monkeypatch.setenv("COCOA_DW_DBUF", "0")
+    b, eb = run(sh, "cocoa+", True, monkeypatch, rounds=4, solver=solver)
+    assert b.plan()["fold"] == "gather" and b.plan()["dw_dbuf"] == 0
+    monkeypatch.delenv("COCOA_DW_DBUF")
+    a, ea = run(sh, "cocoa+", True, monkeypatch, rounds=4, solver=solver)
+    assert a.plan()["fold"] == "blocks" and a.plan()["dw_dbuf"] == 1
+    wb = b.w()
+    assert np.max(np.abs(a.w() - wb)) <= 1e-12 * np.max(np.abs(wb))
+    assert np.max(np.abs(a.alpha() - b.alpha())) <= 1e-12
+    for x, y in zip(ea, eb):
+        assert abs(x["gap"] - y["gap"]) <= 1e-12 * abs(y["primal"]) and x["test_err_count"] == y["test_err_count"]

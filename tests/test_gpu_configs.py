@@ -349,7 +349,9 @@ def test_c4_one_gpu_k1024_fast_vs_oracle(c4_full):
     e = make_engine(sh, strict=False)
     e.init("cocoa+", sh.n_glob, 3, sh.H, sh.lam)
     plan = e.plan()
-    assert plan["solver"] == "chain" and plan["dw_compact"] == 1, plan
+    assert plan["solver"] == "chain" and plan["dw_compact"] == 1 and plan["fold"] == "blocks", plan
+    # four chain workgroups per CU: 1,024 partitions on 256 CUs all resident at once
+    assert plan["lds_bytes"] <= 40 * 1024 and plan["stream_cap"] == 1024 and plan["alpha_lds"] == 0, plan
     run = make_run(sh, od, "cocoa+")
     for t in (1, 2, 3):
         e.round(t)

@@ -592,3 +592,60 @@ def test_eval_async_state_errors(c1):
     s.init("cocoa+", tr.n, 4, 50, 1e-3)
     with pytest.raises(cocoa_amd.CocoaError):
         s.eval_async()  # strict: in line only
+
+
+# ------------------------------------------- in-line eval, deferred read-back --
+@pytest.mark.parametrize("strict", [False, True])
+def test_eval_begin_end_is_bitwise_the_inline_eval(c1, strict):
+    """cocoa_eval_begin / cocoa_eval_end with the next round enqueued in
+    between (the bench's loop): every collected record is bitwise what
+    cocoa_eval returned on a twin engine (strict) or within tolerance (fast:
+    the Gram solver's atomics differ from run to run), and the rounds after it
+    see the same x.w cache (the trajectory continues identically)."""
+    tr, te = c1
+    H = 150
+    a = engine(tr, te, strict=strict)
+    b = engine(tr, te, strict=strict)
+    for e in (a, b):
+        e.init("cocoa+", tr.n, 10, H, 1e-3)
+    inline, deferred = [], []
+    for t in range(1, 7):
+        a.round(t)
+        inline.append(a.eval())
+        b.round(t)
+        if t > 1:
+            deferred.append(b.eval_end())  # round t-1's, read back with round t queued
+        b.eval_begin()
+    deferred.append(b.eval_end())
+    for t, (x, y) in enumerate(zip(inline, deferred), 1):
+        if strict:
+            assert x["primal"].hex() == y["primal"].hex() and x["gap"].hex() == y["gap"].hex(), t
+        else:
+            assert abs(x["gap"] - y["gap"]) <= REL * abs(x["primal"]), t
+        assert x["test_err_count"] == y["test_err_count"], t
+    if strict:
+        assert np.array_equal(a.w(), b.w()) and np.array_equal(a.alpha(), b.alpha())
+    with pytest.raises(cocoa_amd.CocoaError):
+        b.eval_end()  # nothing pending
+    b.eval_begin()
+    with pytest.raises(cocoa_amd.CocoaError):
+        b.eval()  # refused while one is pending
+    b.eval_end()
+
+
+def test_eval_begin_end_on_a_multi_device_context(c1):
+    tr, te = c1
+    g = cocoa_amd.Engine(devices=[0, 0], strict=True)
+    g.set_train(tr)
+    g.set_test(te)
+    one = engine(tr, te, strict=True)
+    for e in (g, one):
+        e.init("cocoa+", tr.n, 4, 50, 1e-3)
+    for t in (1, 2):
+        g.round(t)
+        one.round(t)
+    g.eval_begin()
+    g.round(3)
+    x = g.eval_end()
+    y = one.eval()
+    assert x["gap"].hex() == y["gap"].hex()

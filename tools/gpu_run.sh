@@ -7,6 +7,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of a short bench
 #   pmc              FETCH_SIZE / WRITE_SIZE passes (+ calibration) of the same bench
 #   lines            the C5 / C3 / C4 config lines
+#   lineprof         rocprofv3 --kernel-trace --stats of short C4 / C3 / C5 runs (LINEPROF="c4 c3 ...")
 #   gramprof         Gram-solver wave profile (diag build, tools/prof_gram.py)
 #   ab               the short bench on each library in VARIANTS (names of build/v_NAME; "base" = in-tree)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -53,6 +54,16 @@ for step in "$@"; do
       line c5_localsgd --method localsgd --steps 10 --warmup 2 || exit $?
       line c3 --config c3 --steps 10 --warmup 2 || exit $?
       line c4 --config c4 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+    lineprof)  # rocprofv3 kernel stats of the C3 / C4 / C5 lines (short runs)
+      for cfg in ${LINEPROF:-c4 c3 c5_cocoa}; do
+        case $cfg in
+          c5_*) args="--method ${cfg#c5_}" ;;
+          *) args="--config $cfg" ;;
+        esac
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_${cfg}_$TAG -o run --output-format csv -- \
+          python3 bench.py $args --steps 5 --warmup 1 --no-cpu-baseline --no-gap > $O/rocprof_${cfg}_$TAG.log 2>&1 || exit $?
+        python3 tools/rocprof_stats.py $O/rocprof_${cfg}_$TAG
+      done ;;
     evalab)  # eval kernel variants (COCOA_EVAL_VARIANT) on the C2 bench
       for v in ${EVAL_VARIANTS:-0 1 2}; do
         COCOA_EVAL_VARIANT=$v timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-gap ${BENCH_ARGS} \

@@ -31,7 +31,7 @@ def pick(agg, needle, counter):
 
 
 def main():
-    # tools/pmc_summary.py [SRC_DIR [TAG]]: TAG = the tools/gpu_run.sh TAG of the passes
+    # tools/pmc_summary.py [SRC_DIR [TAG [OUT]]]: TAG = the tools/gpu_run.sh TAG of the passes
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out")
     sfx = "_" + sys.argv[2] if len(sys.argv) > 2 else ""
     f, w = load(os.path.join(src, "pmc_FETCH_SIZE" + sfx)), load(os.path.join(src, "pmc_WRITE_SIZE" + sfx))
@@ -51,7 +51,8 @@ def main():
             ("solver_dense", "dense_solver_kernel", ()), ("gram", "gram_kernel", ("solver_gram",)),
             ("eval", "eval_stream_kernel", ()), ("eval_dense", "eval_dense_kernel", ()),
             ("plan", "plan_kernel", ()), ("fold", "fold_kernel", ("compact",)),
-            ("fold_compact", "fold_compact_kernel", ()), ("apply", "apply_kernel", ()))
+            ("fold_compact", "fold_compact_kernel", ()), ("fold_blocks", "fold_blocks_kernel", ()),
+            ("apply", "apply_kernel", ()))
     for tag, needle, bad in tags:
         names = sorted({k for (k, c) in f if needle in k and not any(b in k for b in bad)})
         if not names:
@@ -63,7 +64,8 @@ def main():
         out["kernels"][tag] = {"kernel": names[0], "launches": n, "fetch_bytes": fe * 1024 * k_fetch,
                                "write_bytes": wr * 1024 * k_w,
                                "hbm_bytes_per_launch": fe * 1024 * k_fetch + wr * 1024 * k_w}
-    dst = os.path.join(ROOT, "profiles", "traffic.json")
+    # tools/pmc_summary.py SRC TAG [OUT]: another workload's passes (e.g. C4) to their own file
+    dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "traffic.json")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

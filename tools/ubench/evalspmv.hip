@@ -42,6 +42,113 @@ __global__ void final_kernel(const double* p, int blocks, double* out) {
     }
 }
 
+
+// Column-sorted tiles (diagnostic): each tile's entries sorted by column so a
+// gather instruction's lanes share cache lines; pos = the entry's offset from
+// the tile's first entry, so each product lands in its row order slot in LDS.
+typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
+typedef double f64x2_t __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x4_t __attribute__((ext_vector_type(4)));
+struct SortedArgs {
+    const uint16_t* scol;  // sorted columns (train | test, concatenated per side)
+    const uint16_t* spos;
+    const double* sval;
+    const uint16_t* t_scol;
+    const uint16_t* t_spos;
+    const double* t_sval;
+};
+template <int TILE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void eval_sorted_kernel(EvalArgs a, SortedArgs z) {
+    constexpr int UNITS = TILE / (4 * BLOCK);
+    __shared__ double prod[TILE + 4];
+    __shared__ uint16_t roff[TILE + 2];
+    __shared__ double red[BLOCK / 64];
+    const int tid = threadIdx.x;
+    const int sub = tid & 15, grp = tid >> 4;
+    double hinge = 0.0, err = 0.0;
+    const int64_t ntiles = a.n_tiles + a.n_t_tiles;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const bool test = t >= a.n_tiles;
+        const int64_t tt = test ? t - a.n_tiles : t;
+        const int64_t* tl = test ? a.t_tiles : a.tiles;
+        const int64_t* te = tl + (test ? a.n_t_tiles : a.n_tiles) + 1;
+        const int64_t* rp = test ? a.t_row_ptr : a.row_ptr;
+        const uint16_t* sc = test ? z.t_scol : z.scol;
+        const uint16_t* sp = test ? z.t_spos : z.spos;
+        const double* sv = test ? z.t_sval : z.sval;
+        const double* yy = test ? a.t_y : a.y;
+        const int64_t r0 = tl[tt], r1 = tl[tt + 1];
+        const int64_t e0 = te[tt], e1 = te[tt + 1];
+        const int nr = (int)(r1 - r0);
+        for (int i = tid; i <= nr; i += BLOCK) roff[i] = (uint16_t)(rp[r0 + i] - e0);
+        const int64_t base = e0 & ~(int64_t)3;
+        const int sh = (int)(e0 - base);
+        const int64_t span = e1 - base;
+        u16x4_t c[UNITS + 1], q[UNITS + 1];
+        f64x2_t v0[UNITS + 1], v1[UNITS + 1];
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            c[u] = u16x4_t{0, 0, 0, 0};
+            q[u] = c[u];
+            v0[u] = f64x2_t{0.0, 0.0};
+            v1[u] = v0[u];
+            if (k < span) {
+                c[u] = __builtin_nontemporal_load((const u16x4_t*)(sc + base + k));
+                q[u] = __builtin_nontemporal_load((const u16x4_t*)(sp + base + k));
+                v0[u] = __builtin_nontemporal_load((const f64x2_t*)(sv + base + k));
+                v1[u] = __builtin_nontemporal_load((const f64x2_t*)(sv + base + k + 2));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            // entries of the unit inside [e0, e1): pos is their row-order offset from e0
+            if (k < span) {
+                const double p0 = v0[u].x * a.w[c[u].x], p1 = v0[u].y * a.w[c[u].y];
+                const double p2 = v1[u].x * a.w[c[u].z], p3 = v1[u].y * a.w[c[u].w];
+                if (k + 0 >= sh && k + 0 < span) prod[q[u].x] = p0;
+                if (k + 1 >= sh && k + 1 < span) prod[q[u].y] = p1;
+                if (k + 2 >= sh && k + 2 < span) prod[q[u].z] = p2;
+                if (k + 3 >= sh && k + 3 < span) prod[q[u].w] = p3;
+            }
+        }
+        __syncthreads();
+        for (int r = grp; r < nr; r += BLOCK / 16) {
+            const int b = roff[r], e = roff[r + 1];
+            double acc = 0.0;
+            for (int qq = b + sub; qq < e; qq += 16) acc += prod[qq];
+            const double dot = cocoa::row16_sum(acc);
+            if (sub == 0) {
+                if (!test) {
+                    hinge += cocoa::jmax(1 - yy[r0 + r] * dot, 0.0);
+                    if (a.row_xw) a.row_xw[r0 + r] = dot;
+                } else {
+                    err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t gt = (int64_t)blockIdx.x * BLOCK + tid;
+    const int64_t gs = (int64_t)gridDim.x * BLOCK;
+    double al = 0.0, w2 = 0.0;
+    for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
+    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
+    double s4[4] = {hinge, al, w2, err};
+    for (int i = 0; i < 4; ++i) {
+        double v = cocoa::wave_sum(s4[i]);
+        __syncthreads();
+        if ((tid & 63) == 0) red[tid >> 6] = v;
+        __syncthreads();
+        double acc = 0.0;
+        for (int j = 0; j < BLOCK / 64; ++j) acc += red[j];
+        s4[i] = acc;
+    }
+    if (tid == 0)
+        for (int i = 0; i < 4; ++i) a.partials[(size_t)blockIdx.x * 4 + i] = s4[i];
+}
+
 template <class T>
 static T* dev(const std::vector<T>& h, size_t pad_bytes = 64) {
     T* p = nullptr;
@@ -195,7 +302,9 @@ int main(int argc, char** argv) {
     };
 
     {  // shipped kernel
-        const auto t4 = tiles(tr.rp, 4096, 4096), tt4 = tiles(te.rp, 4096, 4096);
+        // the library's tile size for this variant (COCOA_EVAL_VARIANT 6-9: 2,048)
+        const int64_t cap = (ev && std::atoi(ev) >= 6 && std::atoi(ev) <= 9) ? 2048 : 4096;
+        const auto t4 = tiles(tr.rp, cap, cap), tt4 = tiles(te.rp, cap, cap);
         EvalArgs b = a;
         b.tiles = dev(t4);
         b.n_tiles = (int64_t)t4.size() / 2 - 1;
@@ -224,6 +333,45 @@ int main(int argc, char** argv) {
         std::snprintf(nm, sizeof nm, "%s U%d b%d x%d", name, U, block, blocks_per_cu);
         check(nm, ms);
     };
+    {  // column-sorted 4,096-entry tiles
+        const auto t4 = tiles(tr.rp, 4096, 4096), tt4 = tiles(te.rp, 4096, 4096);
+        auto sorted = [&](const Side& sd, const std::vector<int64_t>& tl, std::vector<uint16_t>& sc,
+                          std::vector<uint16_t>& sp, std::vector<double>& sv) {
+            const size_t nnz = sd.val.size();
+            sc.assign(nnz, 0);
+            sp.assign(nnz, 0);
+            sv.assign(nnz, 0.0);
+            const size_t nt = tl.size() / 2 - 1;
+            std::vector<int> idx;
+            for (size_t i = 0; i < nt; ++i) {
+                const int64_t e0 = tl[nt + 1 + i], e1 = tl[nt + 1 + i + 1];
+                idx.resize((size_t)(e1 - e0));
+                std::iota(idx.begin(), idx.end(), 0);
+                std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return sd.col16[e0 + x] < sd.col16[e0 + y]; });
+                for (int64_t q = 0; q < e1 - e0; ++q) {
+                    sc[e0 + q] = sd.col16[e0 + idx[q]];
+                    sp[e0 + q] = (uint16_t)idx[q];
+                    sv[e0 + q] = sd.val[e0 + idx[q]];
+                }
+            }
+        };
+        std::vector<uint16_t> sc, sp, tsc, tsp;
+        std::vector<double> sv, tsv;
+        sorted(tr, t4, sc, sp, sv);
+        sorted(te, tt4, tsc, tsp, tsv);
+        SortedArgs z{dev(sc), dev(sp), dev(sv), dev(tsc), dev(tsp), dev(tsv)};
+        EvalArgs b = a;
+        b.tiles = dev(t4);
+        b.n_tiles = (int64_t)t4.size() / 2 - 1;
+        b.t_tiles = dev(tt4);
+        b.n_t_tiles = (int64_t)tt4.size() / 2 - 1;
+        const int nb = 768;
+        const float ms = timeit([&] {
+            eval_sorted_kernel<4096, 512><<<nb, 512, 0, s>>>(b, z);
+            final_kernel<<<1, 64, 0, s>>>(b.partials, nb, b.out);
+        });
+        check("column-sorted tiles 4096", ms);
+    }
     run_wave("wave", eval_wave_kernel<4, 512, true>, 4, 512, 2);
     run_wave("wave", eval_wave_kernel<4, 256, true>, 4, 256, 4);
     run_wave("wave", eval_wave_kernel<2, 512, true>, 2, 512, 3);
