@@ -514,14 +514,16 @@ def test_dense_rows_double_stream(method, strict):
     entry stream and keeps alpha in HBM.  Strict stays bitwise, fast within
     1e-9 of the oracle."""
     rng = np.random.default_rng(5)
-    n, d = 3200, 1500                    # 1,600-row partitions: alpha no longer fits next to the stream
+    # 6,000-row partitions: alpha (48 KB) no longer fits next to the doubled stream
+    # and the LDS-resident vector
+    n, d = 12000, 1500
     z = rng.integers(900, 1500, size=n)
     cols = [np.sort(rng.choice(d, size=int(k), replace=False)).astype(np.int32) for k in z]
     vals = [rng.standard_normal(int(k)) / np.sqrt(k) for k in z]
     row_ptr = np.concatenate([[0], np.cumsum(z)]).astype(np.int64)
     y = np.where(rng.random(n) < 0.5, 1.0, -1.0)
     tr = LabeledData(row_ptr, np.concatenate(cols), np.concatenate(vals), y,
-                     np.array([0, 1600, 3200], np.int64), d)
+                     np.array([0, 6000, 12000], np.int64), d)
     e = engine(tr, strict=strict)
     e.init(method, n, 4, 100, 1e-3, 1.0, 1.0, 1, 3)
     plan = e.plan()

@@ -19,8 +19,8 @@ SHORT="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-gap ${BENCH_
 
 line() {  # name, args...
   local n=$1; shift
-  timeout -k 10 600 python3 bench.py "$@" > $O/line_$n.json 2> $O/line_$n.err || return $?
-  python3 -c "import json;d=json.loads(open('$O/line_$n.json').readlines()[-1]);print('$n', round(d['ms_per_step'],3), '%.4g'%d['value'], d['plan']['solver'], d.get('time_to_gap_s'), d.get('rounds_to_gap'), d['kernel_ms'])"
+  timeout -k 10 600 python3 bench.py "$@" > $O/line_${n}_$TAG.json 2> $O/line_${n}_$TAG.err || return $?
+  python3 -c "import json;d=json.loads(open('$O/line_${n}_$TAG.json').readlines()[-1]);print('$n', round(d['ms_per_step'],3), '%.4g'%d['value'], d['plan']['solver'], d.get('time_to_gap_s'), d.get('rounds_to_gap'), d['kernel_ms'], 'frac', round(d['roofline']['frac'],3), round(d['roofline_eval']['frac'],3))"
 }
 
 for step in "$@"; do
@@ -48,11 +48,11 @@ for step in "$@"; do
           > $O/calib_${c}_$TAG.log 2>&1 || exit $?
       done ;;
     lines)
-      line c5_cocoa --method cocoa --steps 10 --warmup 2 || exit $?
-      line c5_mbcd --method mbcd --steps 10 --warmup 2 || exit $?
-      line c5_mbsgd --method mbsgd --steps 10 --warmup 2 || exit $?
-      line c5_localsgd --method localsgd --steps 10 --warmup 2 || exit $?
-      line c3 --config c3 --steps 10 --warmup 2 || exit $?
+      line c5_cocoa --method cocoa --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
+      line c5_mbcd --method mbcd --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
+      line c5_mbsgd --method mbsgd --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
+      line c5_localsgd --method localsgd --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
+      line c3 --config c3 --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
       line c4 --config c4 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
     lineprof)  # rocprofv3 kernel stats of the C3 / C4 / C5 lines (short runs)
       for cfg in ${LINEPROF:-c4 c3 c5_cocoa}; do

@@ -149,6 +149,119 @@ __global__ __launch_bounds__(BLOCK) void eval_sorted_kernel(EvalArgs a, SortedAr
         for (int i = 0; i < 4; ++i) a.partials[(size_t)blockIdx.x * 4 + i] = s4[i];
 }
 
+
+// Split CSR (diagnostic): each row's entries of the HOT most frequent columns
+// in one CSR, the rest in another; w[0, HOT) in LDS, so the hot entries issue
+// no texture-addresser gather.  One tile = whole rows, both segments loaded
+// 4 entries per lane, products parked in LDS (hot segment, then cold), and
+// 16-lane groups sum each row over its two segments.
+struct SplitArgs {
+    const int64_t* rph;  const uint16_t* ch; const double* vh;   // hot CSR (train)
+    const int64_t* rpc;  const uint16_t* cc; const double* vc;   // cold CSR (train)
+    const int64_t* trph; const uint16_t* tch; const double* tvh; // test
+    const int64_t* trpc; const uint16_t* tcc; const double* tvc;
+};
+template <int TILE, int BLOCK, int HOT>
+__global__ __launch_bounds__(BLOCK) void eval_split_kernel(EvalArgs a, SplitArgs z) {
+    constexpr int UN = TILE / (4 * BLOCK) + 1;  // units per segment per thread (alignment adds one)
+    __shared__ double whot[HOT];
+    __shared__ double prod[TILE + 16];  // hot + cold entries of a tile <= TILE (+ alignment)
+    __shared__ uint16_t roh[TILE + 2], roc[TILE + 2];
+    __shared__ double red[BLOCK / 64];
+    const int tid = threadIdx.x;
+    const int sub = tid & 15, grp = tid >> 4;
+    for (int j = tid; j < HOT; j += BLOCK) whot[j] = a.w[j];
+    __syncthreads();
+    double hinge = 0.0, err = 0.0;
+    const int64_t ntiles = a.n_tiles + a.n_t_tiles;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const bool test = t >= a.n_tiles;
+        const int64_t tt = test ? t - a.n_tiles : t;
+        const int64_t* tl = test ? a.t_tiles : a.tiles;
+        const int64_t* rph = test ? z.trph : z.rph;
+        const int64_t* rpc = test ? z.trpc : z.rpc;
+        const uint16_t* ch = test ? z.tch : z.ch;
+        const uint16_t* cc = test ? z.tcc : z.cc;
+        const double* vh = test ? z.tvh : z.vh;
+        const double* vc = test ? z.tvc : z.vc;
+        const double* yy = test ? a.t_y : a.y;
+        const int64_t r0 = tl[tt], r1 = tl[tt + 1];
+        const int nr = (int)(r1 - r0);
+        const int64_t eh0 = rph[r0], eh1 = rph[r1], ec0 = rpc[r0], ec1 = rpc[r1];
+        const int64_t bh = eh0 & ~(int64_t)3, bc = ec0 & ~(int64_t)3;
+        const int shh = (int)(eh0 - bh), shc = (int)(ec0 - bc);
+        const int sph = (int)(eh1 - bh), spc = (int)(ec1 - bc);
+        const int offc = (sph + 3) & ~3;  // cold products after the hot ones, 16-B aligned
+        for (int i = tid; i <= nr; i += BLOCK) {
+            roh[i] = (uint16_t)(rph[r0 + i] - eh0 + shh);
+            roc[i] = (uint16_t)(rpc[r0 + i] - ec0 + shc + offc);
+        }
+        u16x4_t hc[UN], ccol[UN];
+        f64x2_t h0[UN], h1[UN], c0[UN], c1[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const int k = 4 * (u * BLOCK + tid);
+            hc[u] = ccol[u] = u16x4_t{0, 0, 0, 0};
+            h0[u] = h1[u] = c0[u] = c1[u] = f64x2_t{0.0, 0.0};
+            if (k < sph) {
+                hc[u] = __builtin_nontemporal_load((const u16x4_t*)(ch + bh + k));
+                h0[u] = __builtin_nontemporal_load((const f64x2_t*)(vh + bh + k));
+                h1[u] = __builtin_nontemporal_load((const f64x2_t*)(vh + bh + k + 2));
+            }
+            if (k < spc) {
+                ccol[u] = __builtin_nontemporal_load((const u16x4_t*)(cc + bc + k));
+                c0[u] = __builtin_nontemporal_load((const f64x2_t*)(vc + bc + k));
+                c1[u] = __builtin_nontemporal_load((const f64x2_t*)(vc + bc + k + 2));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            const int k = 4 * (u * BLOCK + tid);
+            if (k < sph) {
+                *(f64x2_t*)(prod + k) = f64x2_t{h0[u].x * whot[min((int)hc[u].x, HOT - 1)], h0[u].y * whot[min((int)hc[u].y, HOT - 1)]};
+                *(f64x2_t*)(prod + k + 2) = f64x2_t{h1[u].x * whot[min((int)hc[u].z, HOT - 1)], h1[u].y * whot[min((int)hc[u].w, HOT - 1)]};
+            }
+            if (k < spc) {
+                *(f64x2_t*)(prod + offc + k) = f64x2_t{c0[u].x * a.w[ccol[u].x], c0[u].y * a.w[ccol[u].y]};
+                *(f64x2_t*)(prod + offc + k + 2) = f64x2_t{c1[u].x * a.w[ccol[u].z], c1[u].y * a.w[ccol[u].w]};
+            }
+        }
+        __syncthreads();
+        for (int r = grp; r < nr; r += BLOCK / 16) {
+            double acc = 0.0;
+            for (int q = roh[r] + sub; q < roh[r + 1]; q += 16) acc += prod[q];
+            for (int q = roc[r] + sub; q < roc[r + 1]; q += 16) acc += prod[q];
+            const double dot = cocoa::row16_sum(acc);
+            if (sub == 0) {
+                if (!test) {
+                    hinge += cocoa::jmax(1 - yy[r0 + r] * dot, 0.0);
+                    if (a.row_xw) a.row_xw[r0 + r] = dot;
+                } else {
+                    err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t gt = (int64_t)blockIdx.x * BLOCK + tid;
+    const int64_t gs = (int64_t)gridDim.x * BLOCK;
+    double al = 0.0, w2 = 0.0;
+    for (int64_t i = gt; i < a.n; i += gs) al += a.alpha[i];
+    for (int64_t j = gt; j < a.d; j += gs) w2 += a.w[j] * a.w[j];
+    double s4[4] = {hinge, al, w2, err};
+    for (int i = 0; i < 4; ++i) {
+        double v = cocoa::wave_sum(s4[i]);
+        __syncthreads();
+        if ((tid & 63) == 0) red[tid >> 6] = v;
+        __syncthreads();
+        double acc = 0.0;
+        for (int j = 0; j < BLOCK / 64; ++j) acc += red[j];
+        s4[i] = acc;
+    }
+    if (tid == 0)
+        for (int i = 0; i < 4; ++i) a.partials[(size_t)blockIdx.x * 4 + i] = s4[i];
+}
+
 template <class T>
 static T* dev(const std::vector<T>& h, size_t pad_bytes = 64) {
     T* p = nullptr;
@@ -371,6 +484,49 @@ int main(int argc, char** argv) {
             final_kernel<<<1, 64, 0, s>>>(b.partials, nb, b.out);
         });
         check("column-sorted tiles 4096", ms);
+    }
+    {  // split CSR: hot columns' entries (w in LDS) and the rest
+        auto split = [&](const Side& sd, int hot, std::vector<int64_t>& rh, std::vector<uint16_t>& ch,
+                         std::vector<double>& vh, std::vector<int64_t>& rc, std::vector<uint16_t>& cc,
+                         std::vector<double>& vc) {
+            rh.assign(1, 0);
+            rc.assign(1, 0);
+            ch.clear(); vh.clear(); cc.clear(); vc.clear();
+            for (size_t r = 0; r + 1 < sd.rp.size(); ++r) {
+                for (int64_t q = sd.rp[r]; q < sd.rp[r + 1]; ++q) {
+                    if (sd.col16[q] < hot) { ch.push_back(sd.col16[q]); vh.push_back(sd.val[q]); }
+                    else { cc.push_back(sd.col16[q]); vc.push_back(sd.val[q]); }
+                }
+                rh.push_back((int64_t)ch.size());
+                rc.push_back((int64_t)cc.size());
+            }
+        };
+        auto run_split = [&](const char* name, auto kern, int hot, int tile, int block, int nb) {
+            std::vector<int64_t> rh, rc, trh, trc;
+            std::vector<uint16_t> ch, cc, tch, tcc;
+            std::vector<double> vh, vc, tvh, tvc;
+            split(tr, hot, rh, ch, vh, rc, cc, vc);
+            split(te, hot, trh, tch, tvh, trc, tcc, tvc);
+            SplitArgs z{dev(rh), dev(ch), dev(vh), dev(rc), dev(cc), dev(vc),
+                        dev(trh), dev(tch), dev(tvh), dev(trc), dev(tcc), dev(tvc)};
+            const auto t4 = tiles(tr.rp, tile, tile), tt4 = tiles(te.rp, tile, tile);
+            EvalArgs b = a;
+            b.tiles = dev(t4);
+            b.n_tiles = (int64_t)t4.size() / 2 - 1;
+            b.t_tiles = dev(tt4);
+            b.n_t_tiles = (int64_t)tt4.size() / 2 - 1;
+            const float ms = timeit([&] {
+                kern<<<nb, block, 0, s>>>(b, z);
+                final_kernel<<<1, 64, 0, s>>>(b.partials, nb, b.out);
+            });
+            check(name, ms);
+        };
+        run_split("split hot2048 t4096 b512x2", eval_split_kernel<4096, 512, 2048>, 2048, 4096, 512, 512);
+        run_split("split hot4096 t4096 b512x2", eval_split_kernel<4096, 512, 4096>, 4096, 4096, 512, 512);
+        run_split("split hot2048 t2048 b256x4", eval_split_kernel<2048, 256, 2048>, 2048, 2048, 256, 1024);
+        run_split("split hot4096 t2048 b256x3", eval_split_kernel<2048, 256, 4096>, 4096, 2048, 256, 768);
+        run_split("split hot1024 t2048 b256x5", eval_split_kernel<2048, 256, 1024>, 1024, 2048, 256, 1280);
+        run_split("split hot2048 t2048 b512x3", eval_split_kernel<2048, 512, 2048>, 2048, 2048, 512, 768);
     }
     run_wave("wave", eval_wave_kernel<4, 512, true>, 4, 512, 2);
     run_wave("wave", eval_wave_kernel<4, 256, true>, 4, 256, 4);
