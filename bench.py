@@ -101,6 +101,8 @@ def main():
                     help="bound on the CPU baseline's fresh run to the gap target")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gap", action="store_true")
+    ap.add_argument("--eval-defer", action="store_true",
+                    help="enqueue round t+1 before reading round t's evaluation back (cocoa_eval_begin / _end)")
     ap.add_argument("--pipeline", action="store_true",
                     help="evaluate each round beside the next one (cocoa_eval_async) instead of in line; measured "
                          "slower on C2 (the next round's plan then forms x.w itself: 0.43 ms vs 0.035)")
@@ -171,9 +173,12 @@ def main():
     def steps(t, count, stop=None):
         """count rounds from t, each evaluated; returns (values, rounds, t_next).
         stop(value) -> True ends the loop at the first round whose value satisfies it.
-        In line (default): round t's evaluation is enqueued behind it
-        (cocoa_eval_begin) and read back (cocoa_eval_end) once round t+1 is
-        queued too, so the GPU does not wait on the host between rounds."""
+        In line (default): cocoa_eval after every round.  --eval-defer: round
+        t's evaluation is enqueued behind it (cocoa_eval_begin) and read back
+        (cocoa_eval_end) once round t+1 is queued too; measured slower on C2
+        (3.40 against 2.9 ms per step): round t+2's Gram rows, enqueued with
+        round t+1 while the evaluation still runs, take the CUs first and the
+        next solver's workgroups (159 KB of LDS each) wait for whole CUs."""
         vals, rounds, pending = [], [], None
         for _ in range(count):
             runner.round(t)
@@ -185,7 +190,7 @@ def main():
                         return vals, rounds, t + 1
                 eng.eval_async()
                 pending = t
-            else:
+            elif args.eval_defer:
                 if pending is not None:
                     vals.append(runner.eval_end()[key])
                     rounds.append(pending)
@@ -194,9 +199,14 @@ def main():
                         return vals, rounds, t + 1
                 runner.eval_begin()
                 pending = t
+            else:
+                vals.append(runner.eval()[key])
+                rounds.append(t)
+                if stop and stop(vals[-1]):
+                    return vals, rounds, t + 1
             t += 1
         if pending is not None:
-            vals.append(eng.eval_wait()[key] if pipe else runner.eval_end()[key])
+            vals.append(eng.eval_wait()[key] if pipe else runner.eval_end()[key])  # (defer only)
             rounds.append(pending)
         return vals, rounds, t
 

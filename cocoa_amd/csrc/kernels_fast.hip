@@ -7,6 +7,7 @@
 #include "kernels.h"
 #include "plan_impl.h"
 #include "solver_dense.h"
+#include "gram_strip.h"
 #include "solver_gram.h"
 #include "solver_impl.h"
 #include "wave.h"
@@ -30,12 +31,22 @@ size_t gram_solver_lds(int64_t d, int32_t* hot) {
     return base + sizeof(double) * (size_t)h;
 }
 
+#ifndef COCOA_GRAM_STRIP
+#define COCOA_GRAM_STRIP 0
+#endif
 void launch_gram(const GramArgs& a, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sizeof(GramLds));
+        (void)hipFuncSetAttribute((const void*)gram_strip_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(GramStripLds));
         attr = true;
+    }
+    if (COCOA_GRAM_STRIP) {  // one workgroup per (partition, strip of kGSB batches), gram_strip.h
+        const int64_t grid = (int64_t)a.K * ((a.nbatch + kGSB - 1) / kGSB);
+        if (grid > 0) gram_strip_kernel<<<(unsigned)grid, kGSThreads, sizeof(GramStripLds), s>>>(a);
+        return;
     }
     const int64_t grid = (int64_t)a.K * a.nbatch;
     if (grid > 0) gram_kernel<<<(unsigned)grid, kGramThreads, sizeof(GramLds), s>>>(a);
