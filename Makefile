@@ -59,7 +59,7 @@ variant:
 	    build/v_$(V)/en.o $(BUILD)/dataset.o $(BUILD)/comm.o $(BUILD)/ingest.strict.o -lpthread -ldl
 
 # PMC calibration / latency micro-benchmarks (tools/gpu_run.sh pmc)
-ubench: tools/ubench/calib tools/ubench/lat tools/ubench/ldsdma tools/ubench/dma_layout tools/ubench/evalspmv
+ubench: tools/ubench/calib tools/ubench/lat tools/ubench/ldsdma tools/ubench/dma_layout tools/ubench/evalspmv tools/ubench/cumask
 # eval-pass variants on the C2 shape (links the library for the generator and the shipped eval)
 tools/ubench/evalspmv: tools/ubench/evalspmv.hip $(CSRC)/eval_wave.h $(OUT)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -ffp-contract=fast -Iinclude -I$(CSRC) $< -o $@.tmp -Lcocoa_amd -lcocoa_hip \

@@ -22,8 +22,8 @@ constexpr int kGSP = kGSU + kGW - kGB;       // partner rows of the strip's wind
 constexpr int kGSThreads = 1024;             // 16 waves, one workgroup per CU
 constexpr int kGSNU = 6;                     // kGSThreads-entry units in registers (6,144 entries)
 constexpr int kGSCH = kGSNU * kGSThreads;
-constexpr int kGSTile = 2048;                // updater positions per hash tile
-constexpr int kGSTable = 4096;               // hash slots
+constexpr int kGSTile = 4096;                // updater positions per hash tile (32 rows of ~76 entries: one tile)
+constexpr int kGSTable = 8192;               // hash slots
 static_assert(kGSP == 64, "the strip's partners are one wave's lanes");
 static_assert(kGSNU % 2 == 0, "owners packed 4 per word");
 
@@ -39,7 +39,8 @@ struct GramStripLds {
     int32_t pcum[kGSP + 1];
 };
 static_assert(sizeof(GramStripLds) <= 160 * 1024, "gram_strip_kernel LDS");
-static_assert(kGSTable == 4096 && kGSTile <= 32767, "gram_hash bits / int16 list links");
+static_assert(kGSTable == 8192 && kGSTile <= 32767, "gs_hash bits / int16 list links");
+__device__ __forceinline__ uint32_t gs_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 19; }  // 13 bits
 
 __global__ __launch_bounds__(kGSThreads, 1) void gram_strip_kernel(GramArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(kGSThreads, 1) void gram_strip_kernel(GramArgs a) {
                     const int32_t i = q - ta;
                     L.eval[i] = vv[u];
                     L.eu[i] = (int8_t)owner_of(u);
-                    uint32_t h = gram_hash(c) & (kGSTable - 1);
+                    uint32_t h = gs_hash(c) & (kGSTable - 1);
                     for (;;) {
                         const int32_t old = atomicCAS(&L.tkey[h], -1, c);
                         if (old == -1 || old == c) break;
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(kGSThreads, 1) void gram_strip_kernel(GramArgs a) {
                 int32_t key[2], hd[2];
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
-                    h[t] = gram_hash(cc[u0 + t]) & (kGSTable - 1);
+                    h[t] = gs_hash(cc[u0 + t]) & (kGSTable - 1);
                     key[t] = L.tkey[h[t]];
                     hd[t] = L.thead[h[t]];
                 }
