@@ -18,8 +18,8 @@ E_ARG, E_PARSE, E_RANGE, E_IO, E_HIP, E_STATE, E_NODEV = -1, -2, -3, -4, -5, -6,
 
 METHOD_COCOA_PLUS, METHOD_COCOA, METHOD_MBCD, METHOD_MBSGD, METHOD_LOCALSGD = 0, 1, 2, 3, 4
 METHODS = {"cocoa+": 0, "cocoa": 1, "mbcd": 2, "mbsgd": 3, "localsgd": 4}
-K_SAMPLE, K_SOLVER, K_FOLD, K_APPLY, K_EVAL, K_PLAN, K_GRAM = 0, 1, 2, 3, 4, 5, 6
-KERNEL_NAMES = ["sample", "solver", "fold", "apply", "eval", "plan", "gram"]
+K_SAMPLE, K_SOLVER, K_FOLD, K_APPLY, K_EVAL, K_PLAN, K_GRAM, K_XW = 0, 1, 2, 3, 4, 5, 6, 7
+KERNEL_NAMES = ["sample", "solver", "fold", "apply", "eval", "plan", "gram", "xw"]
 SOLVERS = {"auto": 0, "chain": 1, "gram": 2, "dense": 3}
 
 

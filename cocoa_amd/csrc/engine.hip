@@ -247,6 +247,18 @@ struct cocoa_ctx {
     hipStream_t gstream = nullptr;
     hipEvent_t g_ready = nullptr, s_done[2] = {nullptr, nullptr};
     int32_t pre_t = -1, pre_buf = 0;  // round prefetched into buffer pre_buf (-1: none)
+    // x.w of a round's sampled rows by xw_produce_kernel on gstream, beside the
+    // solver (whose loader polls the per-batch flags), when no in-line
+    // evaluation formed them: plan_xw[k * xw_stride + j], flags [K][nbatch]
+    // holding the epoch of the round that published them
+    bool xw_prod = false;
+    bool eval_on_g = false;  // the pipelined evaluation on gstream (COCOA_EVAL_ON_GSTREAM=1)
+    int ncu = 256;      // compute units of the device
+    int side_res = 0;   // CUs kept off the side streams for the solver's workgroups (0: none)
+    DevBuf xw_flag;
+    int32_t xw_epoch = 0;
+    int64_t xw_stride = 0;
+    hipEvent_t e_w = nullptr, e_xw = nullptr;
     void gram_quiesce() {  // no prefetch in flight, none pending
         if (gstream) HIPCHK(hipStreamSynchronize(gstream));
         pre_t = -1;
@@ -348,6 +360,8 @@ struct cocoa_ctx {
             (void)hipEventDestroy(g_ready);
             for (auto e : s_done) (void)hipEventDestroy(e);
         }
+        if (e_w) (void)hipEventDestroy(e_w);
+        if (e_xw) (void)hipEventDestroy(e_xw);
         if (estream) {
             (void)hipStreamSynchronize(estream);
             (void)hipStreamDestroy(estream);
@@ -416,10 +430,38 @@ static void sub_check(int rc, const cocoa_ctx* sub);
     require(!(ctx)->is_group(), COCOA_E_STATE, what " is not available on a multi-device context (it exchanges internally)")
 
 // after a stream synchronisation: a Gram-solver launch that had to abort
+// Side streams (Gram rows and x.w on gstream, the pipelined evaluation on
+// estream) may be kept off the CUs the Gram solver's workgroups need: K_loc
+// workgroups of ~159 KB of LDS each wait for WHOLE free CUs, which a side
+// stream's resident workgroups rarely leave (round t+2's Gram rows enqueued
+// while an evaluation runs took the C2 solver 2.55 -> 2.97 ms).  With
+// COCOA_CU_MASK=1 the side streams' CU mask clears bits [0, 8 ceil(K/8)): bit i
+// lies on XCD i mod 8 (clearing bits 0..63 left 24 of 32 CUs on each of the 8
+// XCDs, tools/ubench/cumask.hip), and the solver's blocks are dealt round
+// robin over the XCDs, ceil(K/8) per XCD.
+static int side_reserve(const cocoa_ctx* c, int ncu) {
+    const bool on = std::getenv("COCOA_CU_MASK") && std::atoi(std::getenv("COCOA_CU_MASK"));
+    if (!on || !c->use_gram || ncu % 8 != 0 || c->K_loc > ncu / 2) return 0;
+    return ((c->K_loc + 7) / 8) * 8;
+}
+static void make_side_stream(hipStream_t* st, int reserve, int ncu, int prio) {
+    if (reserve <= 0) {
+        HIPCHK(hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio));
+        return;
+    }
+    std::vector<uint32_t> m((size_t)(ncu + 31) / 32, 0xFFFFFFFFu);
+    for (int i = 0; i < reserve; ++i) m[(size_t)i / 32] &= ~(1u << (i % 32));
+    if (ncu % 32) m.back() &= (1u << (ncu % 32)) - 1;
+    HIPCHK(hipExtStreamCreateWithCUMask(st, (uint32_t)m.size(), m.data()));
+}
+
 static void check_status(cocoa_ctx* c) {
     if (!c->use_gram || !c->status.p) return;
     int st = 0;
-    HIPCHK(hipMemcpy(&st, c->status.p, sizeof(int), hipMemcpyDeviceToHost));
+    // on the context's stream (the solver's), not the null stream, which would
+    // also wait for the CU-masked side streams (created blocking)
+    HIPCHK(hipMemcpyAsync(&st, c->status.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     if (st) throw Error(COCOA_E_HIP, "local solver: a hand-off between the solver's waves timed out (launch aborted)");
 }
 
@@ -1159,6 +1201,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     // (measured: 46 ms per C4 round on the side stream) only compete with them.
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    ctx->ncu = ncu;
     // every local solver but the dense one reads the column array (and the
     // dense rows of cocoa_set_train_dense have none yet)
     if (ctx->strict || !ctx->use_dense) {
@@ -1184,12 +1227,21 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
             if (free_b > gtb + sizeof(int32_t) * (size_t)ctx->samples_cap + ((size_t)1 << 30)) {
                 ctx->gt2.alloc(gtb);
                 ctx->samples2.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
+                const int res = side_reserve(ctx, ncu);
+                if (ctx->gstream && res != ctx->side_res) {  // another CU reservation: a new stream
+                    HIPCHK(hipStreamSynchronize(ctx->gstream));
+                    HIPCHK(hipStreamDestroy(ctx->gstream));
+                    ctx->gstream = nullptr;
+                }
+                ctx->side_res = res;
                 if (!ctx->gstream) {
                     int lo = 0, hi = 0;  // lowest priority: fills the CUs the solver leaves idle
                     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                    HIPCHK(hipStreamCreateWithPriority(&ctx->gstream, hipStreamNonBlocking, lo));
-                    HIPCHK(hipEventCreateWithFlags(&ctx->g_ready, hipEventDisableTiming));
-                    for (auto& e : ctx->s_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    make_side_stream(&ctx->gstream, res, ncu, lo);
+                    if (!ctx->g_ready) {
+                        HIPCHK(hipEventCreateWithFlags(&ctx->g_ready, hipEventDisableTiming));
+                        for (auto& e : ctx->s_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    }
                 }
             } else {
                 ctx->gt2.free();
@@ -1218,7 +1270,21 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
             ctx->plan_zc.free();
         ctx->plan_y.alloc(steps * sizeof(double));
         ctx->plan_q.alloc(steps * sizeof(double));
-        ctx->plan_xw.alloc(steps * sizeof(double));
+        // (a batch's 16 x.w on one 128-byte line for xw_produce_kernel's hand-off)
+        ctx->xw_stride = ((int64_t)H + 15) & ~(int64_t)15;
+        ctx->plan_xw.alloc(std::max(steps, (size_t)K * (size_t)ctx->xw_stride) * sizeof(double));
+        // COCOA_XW_PRODUCER=0: the plan forms x.w in line instead (A/B, tests)
+        const bool xw_env_off = std::getenv("COCOA_XW_PRODUCER") && !std::atoi(std::getenv("COCOA_XW_PRODUCER"));
+        ctx->xw_prod = ctx->use_gram && ctx->gstream && ctx->gt2.p && !xw_env_off;
+        ctx->eval_on_g = ctx->xw_prod && std::getenv("COCOA_EVAL_ON_GSTREAM") && std::atoi(std::getenv("COCOA_EVAL_ON_GSTREAM"));
+        if (ctx->xw_prod) {
+            ctx->xw_flag.alloc_zero(sizeof(int32_t) * (size_t)K * (size_t)ctx->nbatch, s);
+            ctx->xw_epoch = 0;
+            if (!ctx->e_w) HIPCHK(hipEventCreateWithFlags(&ctx->e_w, hipEventDisableTiming));
+            if (!ctx->e_xw) HIPCHK(hipEventCreateWithFlags(&ctx->e_xw, hipEventDisableTiming));
+        } else {
+            ctx->xw_flag.free();
+        }
         a.plan_beg = ctx->plan_beg.as<int64_t>();
         a.plan_z = ctx->plan_z.as<int32_t>();
         a.plan_y = ctx->plan_y.as<double>();
@@ -1231,6 +1297,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         ctx->plan_y.free();
         ctx->plan_q.free();
         ctx->plan_xw.free();
+        ctx->xw_prod = false;
+        ctx->xw_flag.free();
     }
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = true;
@@ -1295,6 +1363,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         c->zpending[c->zero_owed] = true;
         c->zero_owed = -1;
     }
+    bool produce = false;  // x.w by xw_produce_kernel beside the solver (fold waits on e_xw)
     if (H >= 1) {
         // (samples, Gram rows) of this round: prefetched during the last round's
         // solver (overlap), else computed here
@@ -1346,12 +1415,43 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             pa.py = c->plan_y.as<double>();
             pa.pq = c->plan_q.as<double>();
             pa.xw = c->plan_xw.as<double>();
+            produce = c->xw_prod && overlap && pa.need_xw && !pa.xw_cache &&
+                      (c->method != COCOA_METHOD_LOCALSGD || lsgd_t0 >= 0);  // the Gram solver reads them
+            if (produce) {
+                pa.need_xw = 0;
+                pa.xw = nullptr;
+            }
             c->timed(COCOA_K_PLAN, [&] {
                 if (c->strict)
                     launch_plan_strict(pa, s);
                 else
                     launch_plan_fast(pa, s);
             });
+        }
+        if (produce) {
+            // w and this round's samples are final in stream order here
+            HIPCHK(hipEventRecord(c->e_w, s));
+            HIPCHK(hipStreamWaitEvent(c->gstream, c->e_w, 0));
+            XwArgs xa{};
+            xa.part_ptr = c->part_ptr.as<int64_t>();
+            xa.samples = smp;
+            xa.row_ptr = c->tr.row_ptr.as<int64_t>();
+            xa.col = c->tr.col.as<int32_t>();
+            xa.val = c->tr.val.as<double>();
+            xa.w = c->w.as<double>();
+            xa.xw = c->plan_xw.as<double>();
+            xa.flag = c->xw_flag.as<int32_t>();
+            xa.stride = c->xw_stride;
+            xa.K = K;
+            xa.H = H;
+            xa.nbatch = c->nbatch;
+            xa.epoch = ++c->xw_epoch;
+            require(c->xw_flag.bytes >= sizeof(int32_t) * (size_t)K * (size_t)c->nbatch &&
+                        c->plan_xw.bytes >= sizeof(double) * (size_t)K * (size_t)c->xw_stride,
+                    COCOA_E_STATE, "x.w producer buffers");
+            c->timed_on(c->gstream, COCOA_K_XW, [&] { launch_xw_produce(xa, c->gstream); });
+            HIPCHK(hipEventRecord(c->e_xw, c->gstream));
+            if (c->eval_on_g) eval_fire(c);  // the previous state's pipelined evaluation, next on gstream
         }
         if (c->use_dense) {
             DenseArgs g{};
@@ -1381,6 +1481,10 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.plan_y = c->plan_y.as<double>();
             g.plan_q = c->plan_q.as<double>();
             g.plan_xw = c->plan_xw.as<double>();
+            g.xw_flag = produce ? c->xw_flag.as<int32_t>() : nullptr;
+            g.xw_col = c->tr.col.as<int32_t>();
+            g.xw_epoch = c->xw_epoch;
+            g.xw_stride = produce ? c->xw_stride : H;
             g.col = c->dw_compact ? c->col_local.as<int32_t>() : c->tr.col.as<int32_t>();
             g.val = c->tr.val.as<double>();
             g.alpha = c->alpha.as<double>();
@@ -1464,6 +1568,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         else
             c->comm->chain_recv(c->dw_sum, d, true, s);
     }
+    if (produce) HIPCHK(hipStreamWaitEvent(s, c->e_xw, 0));  // its reads of w are done
     c->timed(COCOA_K_FOLD, [&] {
         if (c->dw_compact && c->n_fitems > 0 && c->dw_dbuf && !chain_init)
             launch_fold_blocks(dws, c->fcol16.as<uint16_t>(), c->fbnd.as<uint32_t>(), c->fitems.as<int32_t>(),
@@ -1676,14 +1781,17 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false) {
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     require(async || !ctx->eval_pending, COCOA_E_STATE,
             "an evaluation is pending: collect it with cocoa_eval_wait first");
-    hipStream_t st = async ? ctx->estream : ctx->stream;
+    // (COCOA_EVAL_ON_GSTREAM=1: the pipelined pass on gstream, behind the x.w
+    // producer and ahead of the next Gram rows, instead of beside them)
+    const bool on_g = async && ctx->eval_on_g && ctx->gstream;
+    hipStream_t st = on_g ? ctx->gstream : async ? ctx->estream : ctx->stream;
     const bool dense_eval = !ctx->strict && ctx->tr_dense && (!ctx->has_test || ctx->te_dense || ctx->te.n == 0) &&
                             dense_eval_fits(ctx->d);
     if (!dense_eval) {  // the CSR passes read the column arrays (on the context's stream)
         ensure_cols(ctx->tr, ctx->d, ctx->stream);
         if (ctx->has_test) ensure_cols(ctx->te, ctx->d, ctx->stream);
     }
-    if (async) HIPCHK(hipStreamWaitEvent(ctx->estream, ctx->e_round, 0));  // the snapshots are taken
+    if (async) HIPCHK(hipStreamWaitEvent(st, ctx->e_round, 0));  // the snapshots are taken
     EvalArgs e{};
     e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     e.col = ctx->tr.col.as<int32_t>();
@@ -1814,7 +1922,7 @@ extern "C" int cocoa_eval_async(cocoa_ctx* ctx) {
     require(!ctx->eval_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_wait first");
     require(!ctx->inl_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_end first");
     if (!ctx->estream) {
-        HIPCHK(hipStreamCreateWithFlags(&ctx->estream, hipStreamNonBlocking));
+        make_side_stream(&ctx->estream, ctx->side_res, ctx->ncu, 0);
         HIPCHK(hipEventCreateWithFlags(&ctx->e_round, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ctx->e_done, hipEventDisableTiming));
     }
@@ -2823,12 +2931,13 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
-                  "\"sum_u\":%lld,\"fold\":\"%s\"}",
+                  "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d}",
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,
                   ctx->dw_dbuf ? 1 : 0, ctx->use_dense ? "dense" : ctx->use_gram ? "gram" : "chain",
                   ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u,
-                  !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather");
+                  !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
+                  ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0);
     CAPI_END(ctx)
 }

@@ -158,6 +158,29 @@ struct GramSolverArgs {
     // epilogue turns the slice's delta-v into deltaW = s (keep wInit + dv) - wInit
     const double* w;
     double lambda, t0;
+    // x.w of step j of partition k at plan_xw[k * xw_stride + j]; with xw_flag the
+    // values come from xw_produce_kernel beside the solver, batch b of
+    // partition k published when xw_flag[k * nbatch + b] == xw_epoch
+    const int32_t* xw_flag;
+    const int32_t* xw_col;    // global column of each entry (x.w formed in the loader: w[xw_col])
+    int32_t xw_epoch;
+    int32_t xw_pad;
+    int64_t xw_stride;
+};
+
+// x.w of the round's sampled rows, produced beside the Gram solver (its loader
+// polls the flags): one 256-thread block per (batch, partition), batch-major
+struct XwArgs {
+    const int64_t* part_ptr;
+    const int32_t* samples;   // K_loc * H
+    const int64_t* row_ptr;
+    const int32_t* col;
+    const double* val;
+    const double* w;
+    double* xw;               // [K][stride], stride a multiple of 16 (one 128-byte line per batch)
+    int32_t* flag;            // [K][nbatch]
+    int64_t stride;
+    int32_t K, H, nbatch, epoch;
 };
 
 // Dense-row local solver (solver_dense.h), fast mode: X is the CSR value array
@@ -228,6 +251,7 @@ void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 // when it fits, else in alpha_work)
 size_t gram_solver_lds(int64_t d, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
+void launch_xw_produce(const XwArgs& a, hipStream_t s);
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s);
 // dense rows: whether d and the largest partition (max_nl rows) fit the kernels
 bool dense_solver_fits(int64_t d, int64_t max_nl);

@@ -7,7 +7,6 @@
 #include "kernels.h"
 #include "plan_impl.h"
 #include "solver_dense.h"
-#include "gram_strip.h"
 #include "solver_gram.h"
 #include "solver_impl.h"
 #include "wave.h"
@@ -31,25 +30,50 @@ size_t gram_solver_lds(int64_t d, int32_t* hot) {
     return base + sizeof(double) * (size_t)h;
 }
 
-#ifndef COCOA_GRAM_STRIP
-#define COCOA_GRAM_STRIP 0
-#endif
 void launch_gram(const GramArgs& a, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sizeof(GramLds));
-        (void)hipFuncSetAttribute((const void*)gram_strip_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sizeof(GramStripLds));
         attr = true;
-    }
-    if (COCOA_GRAM_STRIP) {  // one workgroup per (partition, strip of kGSB batches), gram_strip.h
-        const int64_t grid = (int64_t)a.K * ((a.nbatch + kGSB - 1) / kGSB);
-        if (grid > 0) gram_strip_kernel<<<(unsigned)grid, kGSThreads, sizeof(GramStripLds), s>>>(a);
-        return;
     }
     const int64_t grid = (int64_t)a.K * a.nbatch;
     if (grid > 0) gram_kernel<<<(unsigned)grid, kGramThreads, sizeof(GramLds), s>>>(a);
+}
+
+// x.w of the round's sampled rows beside the Gram solver, so that no evaluation
+// pass has to form them in line before the round (plan_impl.h forms the same
+// sums, 16 lanes per step, when it runs in line).  Block (b, k) of the
+// batch-major grid takes batch b of partition k, one step per 16 lanes; the
+// early batches of every partition land first, on the XCD of the partition's
+// solver workgroup (both grids deal k round robin).  Publication
+// (MI355X_MICROARCH.md, inter-workgroup visibility): plain stores, every wave's
+// vmcnt(0), a barrier, then one lane's agent-scope release and the relaxed
+// agent-scope flag store; the loader polls, then acquires (solver_gram.h).
+__global__ __launch_bounds__(256) void xw_produce_kernel(XwArgs a) {
+    const int k = (int)(blockIdx.x % (unsigned)a.K), b = (int)(blockIdx.x / (unsigned)a.K);
+    const int tid = threadIdx.x, sub = tid & 15;
+    const int32_t j = b * kGB + (tid >> 4);
+    if (j < a.H) {  // whole 16-lane rows: the row sum's DPP stays inside active rows
+        const int64_t r = a.part_ptr[k] + a.samples[(size_t)k * a.H + j];
+        const int64_t q0 = a.row_ptr[r], q1 = a.row_ptr[r + 1];
+        double acc = 0.0;
+        for (int64_t q = q0 + sub; q < q1; q += 16) acc += a.val[q] * a.w[a.col[q]];
+        const double xw = row16_sum(acc);
+        if (sub == 0) a.xw[(size_t)k * a.stride + j] = xw;
+    }
+    vm_drain();
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        vm_drain();
+        __hip_atomic_store(a.flag + (size_t)k * a.nbatch + b, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+void launch_xw_produce(const XwArgs& a, hipStream_t s) {
+    const int64_t grid = (int64_t)a.K * a.nbatch;
+    if (grid > 0) xw_produce_kernel<<<(unsigned)grid, 256, 0, s>>>(a);
 }
 
 template <int MODE, bool HOTLDS, bool PROJ>

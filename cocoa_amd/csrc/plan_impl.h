@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         __builtin_nontemporal_store((int32_t)(e - b), a.z + g);
         __builtin_nontemporal_store(a.y[gr], a.py + g);
         __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
-        __builtin_nontemporal_store(xw, a.xw + g);
+        if (a.xw) __builtin_nontemporal_store(xw, a.xw + g);  // (null: xw_produce_kernel forms x.w)
         if (a.row_zc) {
             typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
             __builtin_nontemporal_store(*(const i32x4*)(a.row_zc + 4 * gr), (i32x4*)(a.zc + 4 * g));

@@ -84,6 +84,7 @@ constexpr int kGW = COCOA_GWIN;          // window slots (steps): slot of step s
 constexpr int kGNB = kGW / kGB;          // batches in the window
 static_assert(kGW % kGB == 0 && kGW <= kGSlots && kGNB >= 2, "window");
 constexpr int kGRing = 8;                // record / coefficient ring (batches)
+constexpr uint64_t kXwPatience = 50000;  // cycles the loader polls x.w flags before forming x.w itself (~25 us)
 #ifndef COCOA_GHOT
 #define COCOA_GHOT 48  // (32: Gram rows 2.35 ms, 40: 2.28, 48: 2.26; r03 A/B)
 #endif
@@ -147,10 +148,24 @@ __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F
 //     updaters' cold entries, filled tile by tile (kGramTile packed positions
 //     of the updater rows at a time); every partner cold entry probes it.
 // Windows longer than the register chunk reload it per tile (same results).
+#ifndef COCOA_GRAM_V2
+#define COCOA_GRAM_V2 1
+#endif
+#if COCOA_GRAM_V2
+// hash tiles hold the updaters' COLD entries only, numbered in position order
+// (a block-wide ballot scan), so a tile of 1,024 covers a typical batch
+// (16 rows x ~76 entries, ~2/3 cold) and the LDS fits three workgroups per CU
+constexpr int kGramTable = 2048;     // hash slots (power of two, 2 x kGramTile)
+constexpr int kGramTile = 1024;      // cold updater entries per hash tile
+constexpr int kGramNU = 8;           // kGramThreads-entry units in registers
+constexpr int kGramWGs = 3;          // workgroups per CU (LDS, and <= 80 VGPRs)
+#else
 constexpr int kGramTable = 4096;     // hash slots (power of two, 2 x kGramTile)
 constexpr int kGramTile = 2048;      // updater positions per hash tile (16 rows of ~128 entries: one tile)
-constexpr int kGramThreads = 512;    // 8 waves: two workgroups (53 KB of LDS each) give 16 waves per CU
 constexpr int kGramNU = 12;          // kGramThreads-entry units in registers
+constexpr int kGramWGs = 2;          // workgroups per CU (LDS)
+#endif
+constexpr int kGramThreads = 512;    // 8 waves
 constexpr int kGramCH = kGramNU * kGramThreads;
 constexpr int kGHotS = kGHot + 1;    // XP row stride (doubles)
 
@@ -164,15 +179,20 @@ struct GramLds {
     int8_t eu[kGramTile];
     int64_t pbeg[kGSlots];
     int32_t pcum[kGSlots + 1];       // packed offsets of the partners
+#if COCOA_GRAM_V2
+    int32_t cpre[kGramNU * (kGramThreads / 64)];  // cold-entry rank of each (unit, wave) in a chunk
+    int32_t ctot;                                 // cold entries of the chunk
+#endif
 };
-static_assert(sizeof(GramLds) * 2 <= 160 * 1024, "gram_kernel LDS: two workgroups per CU");
+static_assert(sizeof(GramLds) * kGramWGs <= 160 * 1024, "gram_kernel LDS: kGramWGs workgroups per CU");
+static_assert(!COCOA_GRAM_V2 || kGramNU * (kGramThreads / 64) == 64, "one lane per (unit, wave) in the rank scan");
 static_assert(kGramThreads == 512, "gram_kernel's hot part gives each of the 8 waves two updaters");
 static_assert(kGramNU % 4 == 0, "gram_kernel probes four units at a time");
 
 __device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 20; }  // 12 bits
-static_assert(kGramTable == 4096 && kGramTile <= 32767, "gram_hash bits / int16 list links");
+static_assert(kGramTable <= 4096 && kGramTile <= 32767, "gram_hash bits / int16 list links");
 
-__global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
+__global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramLds& L = *(GramLds*)lds_raw;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -265,6 +285,59 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
             if (cc[u] >= 0 && cc[u] < kGHot) atomicAdd(&L.XP[owner_of(u)][cc[u]], vv[u]);
     }
     phase(1);
+    auto insert = [&](int32_t i, int u) {  // hash-list entry i of unit u's (cold updater) entry
+        const int32_t c = cc[u];
+        L.eval[i] = vv[u];
+        L.eu[i] = (int8_t)owner_of(u);
+        uint32_t h = gram_hash(c) & (kGramTable - 1);
+        for (;;) {
+            const int32_t old = atomicCAS(&L.tkey[h], -1, c);
+            if (old == -1 || old == c) break;
+            h = (h + 1) & (kGramTable - 1);
+        }
+        L.enext[i] = (int16_t)atomicExch(&L.thead[h], i);
+    };
+#if COCOA_GRAM_V2
+    // cold part, one hash tile of cold updater entries at a time: entry rank =
+    // cold updater entries before it in position order (q = qa + 512 u + tid:
+    // unit, wave, lane), the same in every tile's pass
+    int32_t ncold = 0;
+    for (int32_t ta = 0;; ta += kGramTile) {
+        for (int i = tid; i < kGramTable; i += kGramThreads) {
+            L.tkey[i] = -1;
+            L.thead[i] = -1;
+        }
+        int32_t run = 0;  // cold entries of the chunks before qa
+        for (int32_t qa = 0; qa < Q16; qa += kGramCH) {
+            load(qa);
+            uint64_t m[kGramNU];
+#pragma unroll
+            for (int u = 0; u < kGramNU; ++u) {
+                const int32_t q = qa + u * kGramThreads + tid;
+                m[u] = __ballot(q < Q16 && cc[u] >= kGHot);
+                if (lane == 0) L.cpre[u * (kGramThreads / 64) + wv] = __popcll(m[u]);
+            }
+            __syncthreads();
+            if (wv == 0) {
+                const int32_t v = L.cpre[lane];
+                const int32_t inc = wave_incl_scan(v);
+                L.cpre[lane] = inc - v;
+                if (lane == 63) L.ctot = inc;
+            }
+            __syncthreads();
+            const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+            for (int u = 0; u < kGramNU; ++u) {
+                if ((m[u] >> lane) & 1) {
+                    const int32_t i = run + L.cpre[u * (kGramThreads / 64) + wv] + __popcll(m[u] & below) - ta;
+                    if (i >= 0 && i < kGramTile) insert(i, u);
+                }
+            }
+            run += L.ctot;
+            __syncthreads();  // cpre / ctot of the next chunk
+        }
+        ncold = run;
+#else
     // cold part, one hash tile of updater positions at a time
     for (int32_t ta = 0; ta < Q16; ta += kGramTile) {
         for (int i = tid; i < kGramTable; i += kGramThreads) {
@@ -278,21 +351,10 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
 #pragma unroll
             for (int u = 0; u < kGramNU; ++u) {
                 const int32_t q = qa + u * kGramThreads + tid;
-                const int32_t c = cc[u];
-                if (q >= ta && q < tb && c >= kGHot) {
-                    const int32_t i = q - ta;
-                    L.eval[i] = vv[u];
-                    L.eu[i] = (int8_t)owner_of(u);
-                    uint32_t h = gram_hash(c) & (kGramTable - 1);
-                    for (;;) {
-                        const int32_t old = atomicCAS(&L.tkey[h], -1, c);
-                        if (old == -1 || old == c) break;
-                        h = (h + 1) & (kGramTable - 1);
-                    }
-                    L.enext[i] = (int16_t)atomicExch(&L.thead[h], i);
-                }
+                if (q >= ta && q < tb && cc[u] >= kGHot) insert(q - ta, u);
             }
         }
+#endif
         __syncthreads();
         phase(5);
         // entries of updater rows of column c from i on (list order), into partner pp
@@ -360,6 +422,9 @@ __global__ __launch_bounds__(kGramThreads, 2) void gram_kernel(GramArgs a) {
         }
         __syncthreads();
         phase(6);
+#if COCOA_GRAM_V2
+        if (ta + kGramTile >= ncold) break;
+#endif
     }
     phase(2);
     // hot part: wave wv -> updaters 2 wv, 2 wv + 1, lane = partner
@@ -618,7 +683,54 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         int64_t xbeg = 0;
         double ls = 1.0;   // MODE_LSGD: s before the batch (SGD.scala:119-120), wave-uniform
         int32_t lkeep = 1; //   wInit not yet dropped by a zero shrink
+        // x.w from xw_produce_kernel (beside this launch): at the start of every
+        // 16 batches, 16 lanes poll those batches' flags for at most
+        // kXwPatience cycles, then one agent-scope acquire covers the batches
+        // found published.  A batch not published by then (the launch's first
+        // batches before the producer starts, or a device shared with other
+        // spinning grids) forms its x.w here with the producer's summation, so
+        // the solver never waits on another grid's progress.
+        uint32_t xw_ready = 0;  // bit i: batch (16 floor(b/16) + i) published
+        auto xw_poll = [&](int32_t b) {
+            const int32_t bb = b + (lane & 15);
+            const bool need = lane < 16 && bb < NB;
+            const int32_t* fp = a.xw_flag + (size_t)k * NB + (need ? bb : b);
+            const uint64_t t0 = __builtin_readcyclecounter();
+            uint64_t miss;
+            for (;;) {
+                const int32_t v = __hip_atomic_load(fp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                miss = __ballot(need && v != a.xw_epoch);
+                if (!miss || __builtin_readcyclecounter() - t0 > kXwPatience) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (pw) *pw += __builtin_readcyclecounter() - t0;
+            xw_ready = (uint32_t)(__ballot(need) & ~miss);
+            if (xw_ready) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                vm_drain();
+            }
+        };
+        // x.w of batch b's 16 steps from (xbeg, xz): four steps per pass, one
+        // per 16 lanes, summed as xw_produce_kernel / plan_kernel sum them
+        auto xw_inline = [&]() {
+            double r4[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int s = 4 * p + (lane >> 4);
+                const int64_t qb = __shfl(xbeg, s, 64);
+                const int32_t qz = __shfl(xz, s, 64);
+                double acc = 0.0;
+                for (int32_t q = lane & 15; q < qz; q += 16) acc += a.val[qb + q] * a.w[a.xw_col[qb + q]];
+                r4[p] = row16_sum(acc);
+            }
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const double v = __shfl(r4[p], 16 * (lane & 3), 64);
+                if ((lane >> 2) == p) xxw = v;
+            }
+        };
         auto load = [&](int32_t b) {
+            if (a.xw_flag && (b & 15) == 0) xw_poll(b);
             const int32_t j = b * kGB + i;
             xr = nl;
             xz = 0;
@@ -630,12 +742,13 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 xr = a.samples[g0 + j];
                 xy = a.plan_y[g0 + j];
                 xq = a.plan_q[g0 + j];
-                xxw = a.plan_xw[g0 + j];
+                if (!a.xw_flag || ((xw_ready >> (b & 15)) & 1)) xxw = a.plan_xw[(size_t)k * a.xw_stride + j];
                 xbeg = a.plan_beg[g0 + j];
                 xz = a.plan_z[g0 + j];
 #pragma unroll
                 for (int c = 0; c < kGNC - 1; ++c) xzc[c] = a.plan_zc ? a.plan_zc[4 * (g0 + j) + c] : xz;
             }
+            if (a.xw_flag && !((xw_ready >> (b & 15)) & 1)) xw_inline();  // (wave-uniform)
         };
         load(0);
         // batch b's records and layouts; the Gram rows of batch b-4 (LDS DMA, their

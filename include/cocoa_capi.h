@@ -300,7 +300,8 @@ int cocoa_samples(cocoa_ctx *ctx, int32_t part, int32_t seed_plus_t, int32_t cou
 #define COCOA_K_EVAL 4
 #define COCOA_K_PLAN 5   /* per-round step plan (row offsets, x.w) of the SDCA loaders */
 #define COCOA_K_GRAM 6   /* Gram rows of the round (Gram-window solver) */
-#define COCOA_K_COUNT 7
+#define COCOA_K_XW 7     /* x.w of the round's sampled rows, beside the Gram solver */
+#define COCOA_K_COUNT 8
 /* enable = 1: bracket every launch with HIP events on the context stream. */
 int cocoa_stats_enable(cocoa_ctx *ctx, int enable);
 /* total device milliseconds and launch count per kernel id since last reset */

@@ -127,3 +127,68 @@ def test_gram_is_the_default_on_sparse_rows_dense_on_dense_rows_chain_on_long_ro
     assert g.plan()["solver"] == "chain"
     with pytest.raises(cocoa_amd.IllegalArgumentError):
         cocoa_amd._capi.check(cocoa_amd._capi.lib().cocoa_set_solver(f.h, 9), f.h)
+
+
+def _run_env(monkeypatch, env, tr, method, H, T):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = Engine(strict=False)
+    e.set_train(tr)
+    e.set_solver("gram")
+    e.init(method, tr.n, T, H, 2e-3, 1.0, 0.5 if method == "cocoa+" else 1.0, 1, 7)
+    for t in range(1, T + 1):
+        e.round(t)
+    for k in env:
+        monkeypatch.delenv(k)
+    return e
+
+
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "localsgd"])
+def test_xw_producer_matches_the_inline_plan_and_the_oracle(method, monkeypatch):
+    """Rounds with no evaluation before them take x.w from xw_produce_kernel
+    beside the solver (flags polled by the loader) instead of the in-line plan:
+    the same 16-lane sums, so both runs agree with each other far inside the
+    tolerance and with the oracle within it (CoCoA.scala:159, SGD.scala:113)."""
+    tr = _edge()
+    H, T = 150, 5
+    a = _run_env(monkeypatch, {}, tr, method, H, T)
+    b = _run_env(monkeypatch, {"COCOA_XW_PRODUCER": "0"}, tr, method, H, T)
+    assert a.plan()["xw_producer"] == 1 and b.plan()["xw_producer"] == 0
+    run = oracle.Run(odata(tr), method, tr.n, H, 2e-3, 1.0, 0.5 if method == "cocoa+" else 1.0, seed=7)
+    for t in range(1, T + 1):
+        run.round(t)
+    wr = run.w()
+    for e in (a, b):
+        assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+        if method != "localsgd":
+            assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
+    assert np.max(np.abs(a.w() - b.w())) <= 1e-12 * np.max(np.abs(wr))
+
+
+def test_cu_masked_side_streams_pipelined_eval(monkeypatch):
+    """COCOA_CU_MASK=1: the Gram rows, x.w and pipelined-evaluation streams keep
+    off 8 ceil(K/8) CUs; results are the unmasked ones (oracle tolerance), the
+    pipelined evaluation (cocoa_eval_async) included."""
+    tr = _edge()
+    H, T = 150, 4
+    monkeypatch.setenv("COCOA_CU_MASK", "1")
+    e = Engine(strict=False)
+    e.set_train(tr)
+    e.set_solver("gram")
+    e.init("cocoa+", tr.n, T, H, 2e-3, 1.0, 0.5, 1, 7)
+    assert e.plan()["side_cus_reserved"] == 8 and e.plan()["xw_producer"] == 1
+    run = oracle.Run(odata(tr), "cocoa+", tr.n, H, 2e-3, 1.0, 0.5, seed=7)
+    gaps, want = [], []
+    for t in range(1, T + 1):
+        e.round(t)
+        run.round(t)
+        if t > 1:
+            gaps.append(e.eval_wait()["gap"])
+        e.eval_async()
+        want.append(run.eval())
+    gaps.append(e.eval_wait()["gap"])
+    wr = run.w()
+    assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+    assert len(gaps) == T
+    for g, rv in zip(gaps, want):
+        assert abs(g - rv["gap"]) <= REL * abs(rv["primal"])
