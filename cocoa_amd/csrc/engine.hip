@@ -259,6 +259,7 @@ struct cocoa_ctx {
     int32_t xw_epoch = 0;
     int64_t xw_stride = 0;
     hipEvent_t e_w = nullptr, e_xw = nullptr;
+    bool e_w_rec = false;  // e_w recorded behind this round's plan (side work waits on it)
     void gram_quiesce() {  // no prefetch in flight, none pending
         if (gstream) HIPCHK(hipStreamSynchronize(gstream));
         pre_t = -1;
@@ -1428,9 +1429,17 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
                     launch_plan_fast(pa, s);
             });
         }
+        // the side work of this round (x.w producer, a pipelined evaluation)
+        // starts once the plan is done: begun earlier, it slowed the plan (on the
+        // critical path) 0.04 -> 0.2 ms
+        c->e_w_rec = false;
+        if (produce || (c->eval_pending && !c->eval_fired) || overlap) {
+            if (!c->e_w) HIPCHK(hipEventCreateWithFlags(&c->e_w, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(c->e_w, s));
+            c->e_w_rec = true;
+        }
         if (produce) {
             // w and this round's samples are final in stream order here
-            HIPCHK(hipEventRecord(c->e_w, s));
             HIPCHK(hipStreamWaitEvent(c->gstream, c->e_w, 0));
             XwArgs xa{};
             xa.part_ptr = c->part_ptr.as<int64_t>();
@@ -1514,6 +1523,11 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
                 const int nb = 1 - b;
                 if (t < c->P.num_rounds) {
                     HIPCHK(hipStreamWaitEvent(c->gstream, c->s_done[nb], 0));
+                    // and not before this round's plan is done: with the evaluation
+                    // read back after the next round is enqueued (cocoa_eval_begin /
+                    // _end), the Gram rows would otherwise start during that
+                    // evaluation and hold CUs the next solver's workgroups need whole
+                    if (c->e_w_rec) HIPCHK(hipStreamWaitEvent(c->gstream, c->e_w, 0));
                     int32_t* nsmp = nb ? c->samples2.as<int32_t>() : c->samples.as<int32_t>();
                     double* ngt = nb ? c->gt2.as<double>() : c->gt.as<double>();
                     const int32_t nseed = wrap32((int64_t)c->D.seed + t + 1);
@@ -1792,6 +1806,7 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false) {
         if (ctx->has_test) ensure_cols(ctx->te, ctx->d, ctx->stream);
     }
     if (async) HIPCHK(hipStreamWaitEvent(st, ctx->e_round, 0));  // the snapshots are taken
+    if (async && ctx->e_w_rec) HIPCHK(hipStreamWaitEvent(st, ctx->e_w, 0));  // behind this round's plan
     EvalArgs e{};
     e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     e.col = ctx->tr.col.as<int32_t>();

@@ -47,9 +47,12 @@ void launch_gram(const GramArgs& a, hipStream_t s) {
 // batch-major grid takes batch b of partition k, one step per 16 lanes; the
 // early batches of every partition land first, on the XCD of the partition's
 // solver workgroup (both grids deal k round robin).  Publication
-// (MI355X_MICROARCH.md, inter-workgroup visibility): plain stores, every wave's
-// vmcnt(0), a barrier, then one lane's agent-scope release and the relaxed
-// agent-scope flag store; the loader polls, then acquires (solver_gram.h).
+// (MI355X_MICROARCH.md, inter-workgroup visibility, the write-through form):
+// sc1 (agent-scope relaxed) stores, every wave's vmcnt(0), a barrier, then one
+// lane's sc1 flag store; the loader polls the flags and loads the values with
+// sc1 loads (solver_gram.h).  No release fence: an L2 write-back per block
+// (buffer_wbl2) also flushed the solver's freshly dirtied deltaW lines and took
+// the producer to 2.0-2.4 ms and the solver beside it to 4.7 ms (r04m).
 __global__ __launch_bounds__(256) void xw_produce_kernel(XwArgs a) {
     const int k = (int)(blockIdx.x % (unsigned)a.K), b = (int)(blockIdx.x / (unsigned)a.K);
     const int tid = threadIdx.x, sub = tid & 15;
@@ -60,27 +63,35 @@ __global__ __launch_bounds__(256) void xw_produce_kernel(XwArgs a) {
         double acc = 0.0;
         for (int64_t q = q0 + sub; q < q1; q += 16) acc += a.val[q] * a.w[a.col[q]];
         const double xw = row16_sum(acc);
-        if (sub == 0) a.xw[(size_t)k * a.stride + j] = xw;
+        if (sub == 0) __hip_atomic_store(a.xw + (size_t)k * a.stride + j, xw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     vm_drain();
     __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        vm_drain();
+    if (tid == 0)
         __hip_atomic_store(a.flag + (size_t)k * a.nbatch + b, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 void launch_xw_produce(const XwArgs& a, hipStream_t s) {
+    // 4 KB of (unused) LDS: a block then never fits beside a Gram-solver
+    // workgroup (~159 KB), whose issue-bound memory waves it would slow
     const int64_t grid = (int64_t)a.K * a.nbatch;
-    if (grid > 0) xw_produce_kernel<<<(unsigned)grid, 256, 0, s>>>(a);
+    if (grid > 0) xw_produce_kernel<<<(unsigned)grid, 256, 4096, s>>>(a);
 }
 
+template <int MODE, bool HOTLDS, bool PROJ, bool XW>
+static void launch_sg4(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
+    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XW>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    solver_gram_kernel<MODE, HOTLDS, PROJ, XW><<<grid, kGThreads, lds, s>>>(a);
+}
+// XW: the loader takes x.w from xw_produce_kernel's flags (MbCD has no Gram
+// rows, hence no side stream and no producer)
 template <int MODE, bool HOTLDS, bool PROJ>
 static void launch_sg3(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
-    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    solver_gram_kernel<MODE, HOTLDS, PROJ><<<grid, kGThreads, lds, s>>>(a);
+    if (MODE != MODE_MBCD && a.xw_flag)
+        launch_sg4<MODE, HOTLDS, PROJ, MODE != MODE_MBCD>(a, grid, lds, s);
+    else
+        launch_sg4<MODE, HOTLDS, PROJ, false>(a, grid, lds, s);
 }
 template <int MODE, bool HOTLDS>
 static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {

@@ -630,7 +630,7 @@ __device__ __forceinline__ double gram_rule(double u, double aa) {
 //                   the per-class row layouts, up to kGRing batches ahead;
 //   fetch c      -- copy each batch's class-c (column, value) entries into the
 //                   class's LDS sub-ring (LDS DMA), ahead of the gathers.
-template <int MODE, bool HOTLDS, bool PROJ>
+template <int MODE, bool HOTLDS, bool PROJ, bool XW>
 __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramSolverLds& S = *(GramSolverLds*)lds_raw;
@@ -683,14 +683,17 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         int64_t xbeg = 0;
         double ls = 1.0;   // MODE_LSGD: s before the batch (SGD.scala:119-120), wave-uniform
         int32_t lkeep = 1; //   wInit not yet dropped by a zero shrink
-        // x.w from xw_produce_kernel (beside this launch): at the start of every
-        // 16 batches, 16 lanes poll those batches' flags for at most
-        // kXwPatience cycles, then one agent-scope acquire covers the batches
-        // found published.  A batch not published by then (the launch's first
-        // batches before the producer starts, or a device shared with other
-        // spinning grids) forms its x.w here with the producer's summation, so
+        // XW: x.w from xw_produce_kernel (beside this launch).  At the start of
+        // every 16 batches, 16 lanes poll those batches' flags (sc1 loads) for
+        // at most kXwPatience cycles; the batches found published load their x.w
+        // with sc1 loads (the producer stored them sc1, drained, then flagged:
+        // MI355X_MICROARCH.md's write-through hand-off, no acquire).  A batch
+        // not published by then (the launch's first batches before the producer
+        // starts, or a device shared with other spinning grids) forms its x.w
+        // here with the producer's summation when its record is consumed, so
         // the solver never waits on another grid's progress.
         uint32_t xw_ready = 0;  // bit i: batch (16 floor(b/16) + i) published
+        bool xw_miss = false;   // the loaded batch forms its x.w in xw_inline
         auto xw_poll = [&](int32_t b) {
             const int32_t bb = b + (lane & 15);
             const bool need = lane < 16 && bb < NB;
@@ -705,10 +708,6 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             }
             if (pw) *pw += __builtin_readcyclecounter() - t0;
             xw_ready = (uint32_t)(__ballot(need) & ~miss);
-            if (xw_ready) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                vm_drain();
-            }
         };
         // x.w of batch b's 16 steps from (xbeg, xz): four steps per pass, one
         // per 16 lanes, summed as xw_produce_kernel / plan_kernel sum them
@@ -730,7 +729,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             }
         };
         auto load = [&](int32_t b) {
-            if (a.xw_flag && (b & 15) == 0) xw_poll(b);
+            if (XW && (b & 15) == 0) xw_poll(b);
+            if (XW) xw_miss = !((xw_ready >> (b & 15)) & 1);
             const int32_t j = b * kGB + i;
             xr = nl;
             xz = 0;
@@ -742,13 +742,16 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 xr = a.samples[g0 + j];
                 xy = a.plan_y[g0 + j];
                 xq = a.plan_q[g0 + j];
-                if (!a.xw_flag || ((xw_ready >> (b & 15)) & 1)) xxw = a.plan_xw[(size_t)k * a.xw_stride + j];
+                if (!XW)
+                    xxw = a.plan_xw[g0 + j];
+                else if (!xw_miss)
+                    xxw = __hip_atomic_load(const_cast<double*>(a.plan_xw) + (size_t)k * a.xw_stride + j,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 xbeg = a.plan_beg[g0 + j];
                 xz = a.plan_z[g0 + j];
 #pragma unroll
                 for (int c = 0; c < kGNC - 1; ++c) xzc[c] = a.plan_zc ? a.plan_zc[4 * (g0 + j) + c] : xz;
             }
-            if (a.xw_flag && !((xw_ready >> (b & 15)) & 1)) xw_inline();  // (wave-uniform)
         };
         load(0);
         // batch b's records and layouts; the Gram rows of batch b-4 (LDS DMA, their
@@ -774,6 +777,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
 #pragma unroll
                 for (int c = 0; c < kGNC - 1; ++c) ze[c + 1] = xzc[c];
                 ze[kGNC] = z;
+                if (XW && xw_miss) xw_inline();  // (wave-uniform)
                 const double y = xy, q = xq, xw = xxw;
                 const int64_t beg = xbeg;
                 if (b + 1 < NB) load(b + 1);
