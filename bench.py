@@ -101,11 +101,15 @@ def main():
                     help="bound on the CPU baseline's fresh run to the gap target")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gap", action="store_true")
-    ap.add_argument("--eval-defer", action="store_true",
-                    help="enqueue round t+1 before reading round t's evaluation back (cocoa_eval_begin / _end)")
+    ap.add_argument("--stats-all", action="store_true",
+                    help="HIP events around every kernel in the timed region (default: the solver and the eval only)")
+    ap.add_argument("--eval-sync", action="store_true",
+                    help="read each round's evaluation back before enqueuing the next round (cocoa_eval) instead "
+                         "of the default deferred read-back (cocoa_eval_begin / _end)")
     ap.add_argument("--pipeline", action="store_true",
-                    help="evaluate each round beside the next one (cocoa_eval_async) instead of in line; measured "
-                         "slower on C2 (the next round's plan then forms x.w itself: 0.43 ms vs 0.035)")
+                    help="evaluate each round beside the next one (cocoa_eval_async, the next round's x.w from "
+                         "xw_produce_kernel) instead of in line; measured slower on C2 (3.01-3.04 vs 2.90 ms: "
+                         "the side work then outgrows the solver)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     for k in ("n", "d", "nnz", "parts", "lam", "n_test"):
@@ -163,22 +167,25 @@ def main():
         return float(t.item())
 
     # ---- warmup + timed steps ----------------------------------------------
-    # Each round's evaluation in line (cocoa_eval), or with --pipeline (one
-    # device, fast mode) beside the next round (cocoa_eval_async, collected right
-    # after round t+1 is enqueued); either way every evaluation completes inside
-    # the timed region.
+    # Each round's evaluation in line behind it on the engine's stream, read back
+    # once round t+1 is enqueued too (cocoa_eval_begin / _end; --eval-sync: read
+    # back first, cocoa_eval), or with --pipeline (one device, fast mode) beside
+    # the next round (cocoa_eval_async); every evaluation completes inside the
+    # timed region.
     pipe = world == 1 and not args.strict and args.pipeline
+    defer = not pipe and not args.eval_sync
     key = "gap" if sdca else "primal"
 
     def steps(t, count, stop=None):
         """count rounds from t, each evaluated; returns (values, rounds, t_next).
         stop(value) -> True ends the loop at the first round whose value satisfies it.
-        In line (default): cocoa_eval after every round.  --eval-defer: round
-        t's evaluation is enqueued behind it (cocoa_eval_begin) and read back
-        (cocoa_eval_end) once round t+1 is queued too; measured slower on C2
-        (3.40 against 2.9 ms per step): round t+2's Gram rows, enqueued with
-        round t+1 while the evaluation still runs, take the CUs first and the
-        next solver's workgroups (159 KB of LDS each) wait for whole CUs."""
+        Default: round t's evaluation is enqueued behind it (cocoa_eval_begin)
+        and read back (cocoa_eval_end) once round t+1 is queued too, so the GPU
+        never idles while the host reads a gap: 2.895-2.900 against 2.920-2.926
+        ms per C2 step with --eval-sync (cocoa_eval after every round; r04p, one
+        box).  (Round t+2's Gram rows wait for round t+1's plan: enqueued while
+        the evaluation still ran, they took the CUs the next solver's workgroups
+        need whole, 3.40 ms per step in r04f.)"""
         vals, rounds, pending = [], [], None
         for _ in range(count):
             runner.round(t)
@@ -190,7 +197,7 @@ def main():
                         return vals, rounds, t + 1
                 eng.eval_async()
                 pending = t
-            elif args.eval_defer:
+            elif defer:
                 if pending is not None:
                     vals.append(runner.eval_end()[key])
                     rounds.append(pending)
@@ -206,13 +213,17 @@ def main():
                     return vals, rounds, t + 1
             t += 1
         if pending is not None:
-            vals.append(eng.eval_wait()[key] if pipe else runner.eval_end()[key])  # (defer only)
+            vals.append(eng.eval_wait()[key] if pipe else runner.eval_end()[key])
             rounds.append(pending)
         return vals, rounds, t
 
     t = 1
     _, _, t = steps(t, args.warmup)
     eng.stats_reset()
+    # events only around the two kernels the rooflines read: every bracketed
+    # launch adds two event packets and ~5-10 us of launch latency
+    if not args.stats_all and hasattr(cocoa_amd._capi.lib(), "cocoa_stats_kernels"):
+        eng.stats_kernels(["solver", "eval"])
     eng.stats_enable(True)
     barrier()
     ts = time.perf_counter()
@@ -357,6 +368,8 @@ def main():
                        "method": args.method,
                        "n_total": n_glob, "K_total": K_glob, "H": H, "nnz_per_gpu": tr.nnz, "test_rows_per_gpu": te.n,
                        "mode": "strict" if args.strict else "fast",
+                       "eval_flow": "pipelined (cocoa_eval_async)" if pipe else
+                                    "deferred read-back (cocoa_eval_begin/_end)" if defer else "synchronous (cocoa_eval)",
                        "parallelism": f"dp{world}: {tr.num_parts} partitions per GPU, deltaW "
                                       f"{'all-reduce' if not args.strict else 'ordered chain'} inside libcocoa_hip.so "
                                       f"({args.transport.upper()})"},
@@ -370,10 +383,11 @@ def main():
                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach_eval / PEAK_HBM_GBS,
                               "traffic": traffic_eval, "bytes_per_launch": b_eval, "avg_launch_ms": eval_ms,
                               "alone_ms": eval_alone_ms,
-                              "note": "avg_launch_ms: HIP events over the timed rounds (beside the next round's "
-                                      "Gram rows on the side stream" + (" and solver, --pipeline)" if pipe else ")")
+                              "note": "avg_launch_ms: HIP events over the timed rounds (" +
+                                      ("beside the next round's solver and Gram rows, --pipeline)" if pipe else
+                                       "in line on the engine's stream; the next Gram rows wait for the next plan)")
                                       + "; alone_ms: 5 launches after the timed region with nothing beside them"},
-            "kernel_ms": {k: (v["total_ms"] / max(v["launches"], 1)) for k, v in stats.items()},
+            "kernel_ms": {k: (v["total_ms"] / v["launches"]) for k, v in stats.items() if v["launches"] > 0},
             "cpu_baseline": cpu,
             "plan": plan,
         }

@@ -120,6 +120,7 @@ SIGNATURES = {
     "cocoa_local_sdca": (_int, [_vp, _i32, _pf64, _i32, _f64, _i32, _pf64, _i32, _int, _f64, _pf64, _pf64]),
     "cocoa_samples": (_int, [_vp, _i32, _i32, _i32, _pi32]),
     "cocoa_stats_enable": (_int, [_vp, _int]),
+    "cocoa_stats_kernels": (_int, [_vp, ctypes.c_uint32]),
     "cocoa_kernel_stats": (_int, [_vp, _int, _pf64, _pi64]),
     "cocoa_stats_reset": (_int, [_vp]),
     "cocoa_plan_info": (_int, [_vp, ctypes.c_char_p, _int]),
@@ -157,7 +158,9 @@ def lib():
             raise CocoaError(E_NODEV, "libcocoa_hip.so not built: run `make` or __graft_entry__.build()")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
+            f = getattr(L, name, None)
+            if f is None:  # an older library (A/B runs); tests/test_capi_symbols.py checks the shipped one
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L

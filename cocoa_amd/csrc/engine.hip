@@ -226,6 +226,7 @@ struct cocoa_ctx {
     bool proj_rule() const { return alpha_oob || scaling < 0.0 || scaling > 1.0; }
     DevBuf w, alpha, alpha_work, dw, wloc, samples, dw_sum_int, eval_part, eval_out, row_scratch, jump, prof;
     double* dw_sum = nullptr;
+    bool dw_sum_user = false;  // dw_sum is the caller's buffer (cocoa_set_dw_sum_buffer), else dw_sum_int
     double* h_eval = nullptr;  // pinned [4]
     int64_t samples_cap = 0;
 
@@ -277,8 +278,13 @@ struct cocoa_ctx {
     cocoa_eval_result eval_held{};
     bool eval_fired = false;    //   and its kernels enqueued on estream
     DevBuf w_snap, alpha_snap, eval_part2, eval_out2;
+    DevBuf eval_cnt, eval_cnt2;  // last-block counters of the fast sparse pass (in line / pipelined)
     void eval_quiesce();        // the pending evaluation (if any) runs to completion and is dropped
     DevBuf plan_beg, plan_z, plan_zc, plan_y, plan_q, plan_xw;
+    // the next round's step plan (all but x.w), prefetched on gstream beside
+    // this round's solver into the other set (plan set 1 = these)
+    DevBuf plan_beg2, plan_z2, plan_zc2, plan_y2, plan_q2;
+    bool pre_plan = false;  // the prefetched round's plan is in set pre_buf
     // x.w of every train row for the current w, written by the fast eval pass
     // (eval v4) and reused by the next round's plan; false once w moves
     DevBuf row_xw;
@@ -287,6 +293,7 @@ struct cocoa_ctx {
 
     // stats
     bool stats = false;
+    uint32_t stats_mask = ~0u;  // kernel ids bracketed when stats are on (cocoa_stats_kernels)
     struct Pending {
         int kid;
         hipEvent_t a, b;
@@ -312,7 +319,7 @@ struct cocoa_ctx {
     }
     template <class F>
     void timed_on(hipStream_t st, int kid, F&& f) {
-        if (!stats) {
+        if (!stats || !((stats_mask >> kid) & 1)) {
             f();
             HIPCHK(hipGetLastError());
             return;
@@ -1154,7 +1161,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     ctx->samples_cap = std::max<int64_t>((int64_t)K * H, 1);
     ctx->samples.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
     ctx->dw_sum_int.alloc(sizeof(double) * (size_t)d);
-    if (!ctx->dw_sum) ctx->dw_sum = ctx->dw_sum_int.as<double>();
+    // (re-allocated on every init: a pointer kept from an earlier init would dangle)
+    if (!ctx->dw_sum_user) ctx->dw_sum = ctx->dw_sum_int.as<double>();
     ctx->eval_part.alloc(sizeof(double) * (size_t)std::max<int64_t>(4 * 2048, 2 * K + 8));
     ctx->eval_out.alloc(sizeof(double) * 8);
     ctx->row_scratch.alloc(sizeof(double) * (size_t)std::max<int64_t>(n + ctx->te.n, 1));
@@ -1274,6 +1282,23 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         // (a batch's 16 x.w on one 128-byte line for xw_produce_kernel's hand-off)
         ctx->xw_stride = ((int64_t)H + 15) & ~(int64_t)15;
         ctx->plan_xw.alloc(std::max(steps, (size_t)K * (size_t)ctx->xw_stride) * sizeof(double));
+        if (ctx->use_gram && ctx->gt2.p) {  // (the Gram rows' prefetch runs the next plan too)
+            ctx->plan_beg2.alloc(steps * sizeof(int64_t));
+            ctx->plan_z2.alloc(steps * sizeof(int32_t));
+            if (ctx->row_zc.p)
+                ctx->plan_zc2.alloc(steps * 4 * sizeof(int32_t));
+            else
+                ctx->plan_zc2.free();
+            ctx->plan_y2.alloc(steps * sizeof(double));
+            ctx->plan_q2.alloc(steps * sizeof(double));
+        } else {
+            ctx->plan_beg2.free();
+            ctx->plan_z2.free();
+            ctx->plan_zc2.free();
+            ctx->plan_y2.free();
+            ctx->plan_q2.free();
+        }
+        ctx->pre_plan = false;
         // COCOA_XW_PRODUCER=0: the plan forms x.w in line instead (A/B, tests)
         const bool xw_env_off = std::getenv("COCOA_XW_PRODUCER") && !std::atoi(std::getenv("COCOA_XW_PRODUCER"));
         ctx->xw_prod = ctx->use_gram && ctx->gstream && ctx->gt2.p && !xw_env_off;
@@ -1314,6 +1339,30 @@ static bool dw_double_buffer(size_t bytes, bool compact) {
     const char* e = std::getenv("COCOA_DW_DBUF");
     if (e) return std::atoi(e) != 0;
     return compact || bytes >= ((size_t)1 << 30);
+}
+
+// The step plan of the round whose samples are `samples` into plan set `set`
+// (0: plan_*, 1: plan_*2); need_xw / xw_cache / xw as the caller sets them.
+static PlanArgs plan_args(cocoa_ctx* c, const int32_t* samples, int set) {
+    PlanArgs pa{};
+    pa.part_ptr = c->part_ptr.as<int64_t>();
+    pa.samples = samples;
+    pa.row_ptr = c->tr.row_ptr.as<int64_t>();
+    pa.col = c->tr.col.as<int32_t>();
+    pa.val = c->tr.val.as<double>();
+    pa.y = c->tr.y.as<double>();
+    pa.sqn = c->sqn.as<double>();
+    pa.w = c->w.as<double>();
+    pa.steps = (int64_t)c->K_loc * c->P.local_iters;
+    pa.H = c->P.local_iters;
+    pa.row_zc = c->plan_zc.p ? c->row_zc.as<int32_t>() : nullptr;
+    pa.zc = !c->plan_zc.p ? nullptr : set ? c->plan_zc2.as<int32_t>() : c->plan_zc.as<int32_t>();
+    pa.beg = set ? c->plan_beg2.as<int64_t>() : c->plan_beg.as<int64_t>();
+    pa.z = set ? c->plan_z2.as<int32_t>() : c->plan_z.as<int32_t>();
+    pa.py = set ? c->plan_y2.as<double>() : c->plan_y.as<double>();
+    pa.pq = set ? c->plan_q2.as<double>() : c->plan_q.as<double>();
+    pa.xw = c->plan_xw.as<double>();
+    return pa;
 }
 
 static GramArgs gram_args(cocoa_ctx* c, const int32_t* samples, double* gt) {
@@ -1375,6 +1424,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         static const bool serial = std::getenv("COCOA_GRAM_SERIAL") && std::atoi(std::getenv("COCOA_GRAM_SERIAL"));
         const bool overlap = gram_rows && c->gstream && c->gt2.p && !serial;
         int b = 0;
+        const bool plan_ready = overlap && c->pre_t == t && c->pre_plan;  // (set pre_buf)
         if (overlap && c->pre_t == t) {
             b = c->pre_buf;
             HIPCHK(hipStreamWaitEvent(s, c->g_ready, 0));
@@ -1390,44 +1440,42 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             }
         }
         c->pre_t = -1;
+        c->pre_plan = false;
         int32_t* smp = b ? c->samples2.as<int32_t>() : c->samples.as<int32_t>();
         double* gtb = b ? c->gt2.as<double>() : c->gt.as<double>();
         c->sa.samples = smp;
+        // the Gram solver runs this round (local SGD's wrapped-counter rounds do not)
+        const bool gram_round = c->use_gram && (c->method != COCOA_METHOD_LOCALSGD || lsgd_t0 >= 0);
+        bool rows = false;  // x.w gathered from the last evaluation's row cache (the rest prefetched)
         if (c->use_plan) {
-            PlanArgs pa{};
-            pa.part_ptr = c->part_ptr.as<int64_t>();
-            pa.samples = smp;
-            pa.row_ptr = c->tr.row_ptr.as<int64_t>();
-            pa.col = c->tr.col.as<int32_t>();
-            pa.val = c->tr.val.as<double>();
-            pa.y = c->tr.y.as<double>();
-            pa.sqn = c->sqn.as<double>();
-            pa.w = c->w.as<double>();
-            pa.steps = (int64_t)K * H;
-            pa.H = H;
+            PlanArgs pa = plan_args(c, smp, b);
             // CoCoA's w moves inside the round: the chain solver forms x.w itself;
             // the Gram solver splits x.w_local = x.w + x.deltaW
             pa.need_xw = !c->use_dense && (c->method != COCOA_METHOD_COCOA || c->use_gram);
             pa.xw_cache = (c->xw_cached && !c->strict) ? c->row_xw.as<double>() : nullptr;
-            pa.row_zc = c->plan_zc.p ? c->row_zc.as<int32_t>() : nullptr;
-            pa.zc = c->plan_zc.p ? c->plan_zc.as<int32_t>() : nullptr;
-            pa.beg = c->plan_beg.as<int64_t>();
-            pa.z = c->plan_z.as<int32_t>();
-            pa.py = c->plan_y.as<double>();
-            pa.pq = c->plan_q.as<double>();
-            pa.xw = c->plan_xw.as<double>();
-            produce = c->xw_prod && overlap && pa.need_xw && !pa.xw_cache &&
-                      (c->method != COCOA_METHOD_LOCALSGD || lsgd_t0 >= 0);  // the Gram solver reads them
-            if (produce) {
+            rows = gram_round && overlap && pa.need_xw && pa.xw_cache;
+            produce = !rows && c->xw_prod && overlap && pa.need_xw && !pa.xw_cache && gram_round;
+            if (rows || produce) {  // x.w comes from elsewhere: the plan's other fields only
                 pa.need_xw = 0;
                 pa.xw = nullptr;
             }
-            c->timed(COCOA_K_PLAN, [&] {
-                if (c->strict)
-                    launch_plan_strict(pa, s);
-                else
-                    launch_plan_fast(pa, s);
-            });
+            // (the prefetched plan, formed beside the last solver, is exactly that)
+            if (plan_ready && rows) {
+                c->timed(COCOA_K_PLAN, [&] {
+                    launch_xw_gather(pa.part_ptr, smp, H, pa.steps, c->row_xw.as<double>(), c->plan_xw.as<double>(), s);
+                });
+            } else if (!(plan_ready && produce)) {
+                if (rows) {  // one pass: the plan with x.w from the cache
+                    pa.need_xw = 1;
+                    pa.xw = c->plan_xw.as<double>();
+                }
+                c->timed(COCOA_K_PLAN, [&] {
+                    if (c->strict)
+                        launch_plan_strict(pa, s);
+                    else
+                        launch_plan_fast(pa, s);
+                });
+            }
         }
         // the side work of this round (x.w producer, a pipelined evaluation)
         // starts once the plan is done: begun earlier, it slowed the plan (on the
@@ -1484,11 +1532,14 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             GramSolverArgs g{};
             g.part_ptr = c->part_ptr.as<int64_t>();
             g.samples = smp;
-            g.plan_beg = c->plan_beg.as<int64_t>();
-            g.plan_z = c->plan_z.as<int32_t>();
-            g.plan_zc = c->plan_zc.p ? c->plan_zc.as<int32_t>() : nullptr;
-            g.plan_y = c->plan_y.as<double>();
-            g.plan_q = c->plan_q.as<double>();
+            {
+                const PlanArgs ps = plan_args(c, smp, b);  // (this round's plan set)
+                g.plan_beg = ps.beg;
+                g.plan_z = ps.z;
+                g.plan_zc = ps.zc;
+                g.plan_y = ps.py;
+                g.plan_q = ps.pq;
+            }
             g.plan_xw = c->plan_xw.as<double>();
             g.xw_flag = produce ? c->xw_flag.as<int32_t>() : nullptr;
             g.xw_col = c->tr.col.as<int32_t>();
@@ -1534,6 +1585,13 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
                     c->timed_on(c->gstream, COCOA_K_SAMPLE, [&] {
                         launch_sampler(c->part_ptr.as<int64_t>(), K, nseed, H, nsmp, c->jump.as<uint64_t>(), c->gstream);
                     });
+                    if (c->plan_beg2.p) {  // round t+1's plan but x.w, into the other plan set
+                        PlanArgs pn = plan_args(c, nsmp, nb);
+                        pn.need_xw = 0;
+                        pn.xw = nullptr;
+                        c->timed_on(c->gstream, COCOA_K_PLAN, [&] { launch_plan_fast(pn, c->gstream); });
+                        c->pre_plan = true;
+                    }
                     GramArgs ga = gram_args(c, nsmp, ngt);
                     ga.prof = nullptr;
                     c->timed_on(c->gstream, COCOA_K_GRAM, [&] { launch_gram(ga, c->gstream); });
@@ -1619,6 +1677,7 @@ extern "C" int cocoa_set_dw_sum_buffer(cocoa_ctx* ctx, void* device_ptr) {
     CAPI_BEGIN(ctx)
     GROUP_REJECT(ctx, "cocoa_set_dw_sum_buffer");
     ctx->dw_sum = device_ptr ? (double*)device_ptr : ctx->dw_sum_int.as<double>();
+    ctx->dw_sum_user = device_ptr != nullptr;
     CAPI_END(ctx)
 }
 
@@ -1807,6 +1866,7 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false) {
     }
     if (async) HIPCHK(hipStreamWaitEvent(st, ctx->e_round, 0));  // the snapshots are taken
     if (async && ctx->e_w_rec) HIPCHK(hipStreamWaitEvent(st, ctx->e_w, 0));  // behind this round's plan
+    bool host_done = false;  // the sums already stored to h_eval by the pass
     EvalArgs e{};
     e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     e.col = ctx->tr.col.as<int32_t>();
@@ -1838,17 +1898,25 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false) {
             launch_eval_strict(e, st);
         else {
             e.row_xw = async ? nullptr : ctx->row_xw.as<double>();
-            if (dense_eval)
+            if (dense_eval) {
                 launch_eval_dense(e, st);  // rows read as X[n][d]: 8 B per entry
-            else
-                launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), st);
+            } else {
+                // the last block sums the partials and stores them to the pinned
+                // result (no final-sum launch, no copy behind it)
+                DevBuf& cnt = async ? ctx->eval_cnt2 : ctx->eval_cnt;
+                if (!cnt.p) cnt.alloc_zero(sizeof(unsigned), st);
+                e.counter = cnt.as<unsigned>();
+                e.out_host = ctx->h_eval + (async ? 4 : 0);
+                host_done = launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), st);
+            }
             ctx->xw_cached = !async;  // the next round's plan reuses these x.w (stream order)
         }
     });
     if (async) {
-        HIPCHK(hipMemcpyAsync(ctx->h_eval + 4, ctx->eval_out2.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (!host_done)
+            HIPCHK(hipMemcpyAsync(ctx->h_eval + 4, ctx->eval_out2.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
         HIPCHK(hipEventRecord(ctx->e_done, st));
-    } else {
+    } else if (!host_done) {
         HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
     }
 }
@@ -2873,6 +2941,13 @@ extern "C" int cocoa_stats_enable(cocoa_ctx* ctx, int enable) {
     for (cocoa_ctx* sub : ctx->subs) sub_check(cocoa_stats_enable(sub, enable), sub);
     ctx->drain();
     ctx->stats = enable != 0;
+    CAPI_END(ctx)
+}
+
+extern "C" int cocoa_stats_kernels(cocoa_ctx* ctx, uint32_t mask) {
+    CAPI_BEGIN(ctx)
+    for (cocoa_ctx* sub : ctx->subs) sub_check(cocoa_stats_kernels(sub, mask), sub);
+    ctx->stats_mask = mask;
     CAPI_END(ctx)
 }
 

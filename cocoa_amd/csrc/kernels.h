@@ -238,12 +238,18 @@ struct EvalArgs {
     // null; padded like col (the fast eval then streams 10 B per entry)
     const uint16_t* col16;
     const uint16_t* t_col16;
+    // fast sparse pass: with counter (zero between launches) the last block to
+    // finish sums the block partials itself (no eval_final_kernel launch) and
+    // also stores the 4 sums to out_host (pinned) when set
+    unsigned* counter;
+    double* out_host;
 };
 
 // fast translation unit
 void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,
                         hipStream_t s);
-void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
+// returns true when the sums were also stored to a.out_host (no copy needed)
+bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
 int eval_fast_blocks(int64_t n, int64_t n_test);
 int eval_tile_entries();  // entries per fast-eval tile (make_tiles cap)
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
@@ -252,6 +258,8 @@ void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 size_t gram_solver_lds(int64_t d, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
 void launch_xw_produce(const XwArgs& a, hipStream_t s);
+void launch_xw_gather(const int64_t* part_ptr, const int32_t* samples, int32_t H, int64_t steps,
+                      const double* row_xw, double* xw, hipStream_t s);
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s);
 // dense rows: whether d and the largest partition (max_nl rows) fit the kernels
 bool dense_solver_fits(int64_t d, int64_t max_nl);

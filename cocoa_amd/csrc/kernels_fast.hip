@@ -78,20 +78,40 @@ void launch_xw_produce(const XwArgs& a, hipStream_t s) {
     if (grid > 0) xw_produce_kernel<<<(unsigned)grid, 256, 4096, s>>>(a);
 }
 
-template <int MODE, bool HOTLDS, bool PROJ, bool XW>
+template <int MODE, bool HOTLDS, bool PROJ, int XWM>
 static void launch_sg4(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
-    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XW>,
+    (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XWM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    solver_gram_kernel<MODE, HOTLDS, PROJ, XW><<<grid, kGThreads, lds, s>>>(a);
+    solver_gram_kernel<MODE, HOTLDS, PROJ, XWM><<<grid, kGThreads, lds, s>>>(a);
 }
-// XW: the loader takes x.w from xw_produce_kernel's flags (MbCD has no Gram
-// rows, hence no side stream and no producer)
+// the loader's x.w: xw_produce_kernel's flags or the plan's (MbCD has no Gram
+// rows, hence no side stream and no producer: always the plan's).  Measured and
+// not kept (r04s): the loader gathering x.w from the evaluation's per-row cache
+// itself, the sample loaded a batch ahead: solver 2.56 -> 2.90 ms (16 scattered
+// lines per batch on the loader instead of one).
 template <int MODE, bool HOTLDS, bool PROJ>
 static void launch_sg3(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
     if (MODE != MODE_MBCD && a.xw_flag)
-        launch_sg4<MODE, HOTLDS, PROJ, MODE != MODE_MBCD>(a, grid, lds, s);
+        launch_sg4<MODE, HOTLDS, PROJ, MODE != MODE_MBCD ? kXwProducer : kXwPlan>(a, grid, lds, s);
     else
-        launch_sg4<MODE, HOTLDS, PROJ, false>(a, grid, lds, s);
+        launch_sg4<MODE, HOTLDS, PROJ, kXwPlan>(a, grid, lds, s);
+}
+
+// plan_xw[g] = row_xw[part_ptr[k] + samples[g]]: the step plan's x.w from the
+// evaluation's per-row cache, when the rest of the plan was formed beside the
+// previous round
+__global__ __launch_bounds__(256) void xw_gather_kernel(const int64_t* part_ptr, const int32_t* samples, int32_t H,
+                                                        int64_t steps, const double* row_xw, double* xw) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= steps) return;
+    const int64_t r = part_ptr[g / H] + samples[g];
+    __builtin_nontemporal_store(row_xw[r], xw + g);
+}
+
+void launch_xw_gather(const int64_t* part_ptr, const int32_t* samples, int32_t H, int64_t steps,
+                      const double* row_xw, double* xw, hipStream_t s) {
+    if (steps > 0 && H > 0)
+        xw_gather_kernel<<<(unsigned)((steps + 255) / 256), 256, 0, s>>>(part_ptr, samples, H, steps, row_xw, xw);
 }
 template <int MODE, bool HOTLDS>
 static void launch_sg(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
@@ -200,6 +220,31 @@ __device__ __forceinline__ double w_at(const double* w, const double* whot, int3
     return x;
 }
 
+// The block partials' sum in a fixed order (threads [0, 256) of the calling
+// block; every thread of the block calls it): out[0..3], and out_host (system
+// scope) when set.  sc1: the partials were handed over write-through.
+__device__ __forceinline__ void eval_reduce(const double* partials, int blocks, double* out, double* out_host,
+                                            double (*red)[4], bool sc1) {
+    const int tid = threadIdx.x;
+    double v[4] = {0, 0, 0, 0};
+    if (tid < 256)
+        for (int b = tid; b < blocks; b += 256)
+            for (int i = 0; i < 4; ++i) {
+                double* q = const_cast<double*>(partials) + (size_t)b * 4 + i;
+                v[i] += sc1 ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
+            }
+    for (int i = 0; i < 4; ++i) {
+        const double s = wave_sum(v[i]);
+        if ((tid & 63) == 0 && tid < 256) red[i][tid >> 6] = s;
+    }
+    __syncthreads();
+    if (tid < 4) {
+        const double r = ((red[tid][0] + red[tid][1]) + red[tid][2]) + red[tid][3];
+        out[tid] = r;
+        if (out_host) __hip_atomic_store(out_host + tid, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 template <int TILE, int BLOCK, bool C16, int DIAGW = 0, int HOT = 0>
 __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     constexpr int UNITS = TILE / (4 * BLOCK);  // 4-entry units per thread (base alignment adds one)
@@ -299,13 +344,33 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     const double s1 = block_sum_n<BLOCK>(al, red);
     const double s2 = block_sum_n<BLOCK>(w2, red);
     const double s3 = block_sum_n<BLOCK>(err, red);
-    if (tid == 0) {
-        double* p = a.partials + (size_t)blockIdx.x * 4;
-        p[0] = s0;
-        p[1] = s1;
-        p[2] = s2;
-        p[3] = s3;
+    double* p = a.partials + (size_t)blockIdx.x * 4;
+    if (!a.counter) {
+        if (tid == 0) {
+            p[0] = s0;
+            p[1] = s1;
+            p[2] = s2;
+            p[3] = s3;
+        }
+        return;
     }
+    // the last block to finish sums the partials (MI355X_MICROARCH.md's
+    // write-through hand-off: sc1 partials, the storing lane's vmcnt(0), one
+    // agent-scope add per block, sc1 loads by the block whose add came last)
+    __shared__ int last;
+    if (tid == 0) {
+        __hip_atomic_store(p + 0, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p + 2, s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p + 3, s3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vm_drain();
+        last = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __shared__ double red4[4][4];
+    eval_reduce(a.partials, (int)gridDim.x, a.out, a.out_host, red4, true);
+    if (tid == 0) __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
 }
 
 #ifdef COCOA_DIAG
@@ -377,16 +442,7 @@ __global__ __launch_bounds__(256) void eval_rows_kernel(EvalArgs a) {
 
 __global__ __launch_bounds__(256) void eval_final_kernel(const double* partials, int blocks, double* out) {
     __shared__ double red[4][4];
-    const int tid = threadIdx.x;
-    double v[4] = {0, 0, 0, 0};
-    for (int b = tid; b < blocks; b += 256)
-        for (int i = 0; i < 4; ++i) v[i] += partials[(size_t)b * 4 + i];
-    for (int i = 0; i < 4; ++i) {
-        const double s = wave_sum(v[i]);
-        if ((tid & 63) == 0) red[i][tid >> 6] = s;
-    }
-    __syncthreads();
-    if (tid < 4) out[tid] = ((red[tid][0] + red[tid][1]) + red[tid][2]) + red[tid][3];
+    eval_reduce(partials, blocks, out, nullptr, red, false);
 }
 
 // 4,096-entry tiles, 512 threads, 3 blocks per CU (41 KB of LDS per block).
@@ -471,16 +527,19 @@ static bool launch_eval_diag(const EvalArgs& a, bool c16, hipStream_t s) {
 int eval_tile_entries() { return kEvalTile; }
 #endif
 
-void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
+bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
     const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
 #ifdef COCOA_DIAG
-    if (launch_eval_diag(a, c16, s)) return;
+    EvalArgs u = a;
+    u.counter = nullptr;  // the variants end with eval_final_kernel
+    if (launch_eval_diag(u, c16, s)) return false;
 #endif
     if (c16)
         eval_stream_kernel<kEvalTile, 512, true><<<blocks, 512, 0, s>>>(a);
     else
         eval_stream_kernel<kEvalTile, 512, false><<<blocks, 512, 0, s>>>(a);
-    eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+    if (!a.counter) eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+    return a.counter && a.out_host;
 }
 
 // --------------------------------------------- compact fold by blocks --

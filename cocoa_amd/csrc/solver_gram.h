@@ -84,6 +84,7 @@ constexpr int kGW = COCOA_GWIN;          // window slots (steps): slot of step s
 constexpr int kGNB = kGW / kGB;          // batches in the window
 static_assert(kGW % kGB == 0 && kGW <= kGSlots && kGNB >= 2, "window");
 constexpr int kGRing = 8;                // record / coefficient ring (batches)
+constexpr int kXwPlan = 0, kXwProducer = 1;  // solver_gram_kernel's x.w source
 constexpr uint64_t kXwPatience = 50000;  // cycles the loader polls x.w flags before forming x.w itself (~25 us)
 #ifndef COCOA_GHOT
 #define COCOA_GHOT 48  // (32: Gram rows 2.35 ms, 40: 2.28, 48: 2.26; r03 A/B)
@@ -630,8 +631,9 @@ __device__ __forceinline__ double gram_rule(double u, double aa) {
 //                   the per-class row layouts, up to kGRing batches ahead;
 //   fetch c      -- copy each batch's class-c (column, value) entries into the
 //                   class's LDS sub-ring (LDS DMA), ahead of the gathers.
-template <int MODE, bool HOTLDS, bool PROJ, bool XW>
+template <int MODE, bool HOTLDS, bool PROJ, int XWM>
 __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArgs a) {
+    constexpr bool XW = XWM == kXwProducer;  // x.w: plan_xw (kXwPlan) or the producer's flags
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramSolverLds& S = *(GramSolverLds*)lds_raw;
     // LDS after the hand-off state: deltaW of the hot columns [0, a.hot)

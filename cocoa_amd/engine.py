@@ -289,6 +289,11 @@ class Engine:
     def stats_enable(self, on=True):
         C.check(C.lib().cocoa_stats_enable(self.h, 1 if on else 0), self.h)
 
+    def stats_kernels(self, names=None):
+        """Bracket only these kernels (names from KERNEL_NAMES; None: all) while stats are on."""
+        mask = 0xFFFFFFFF if names is None else sum(1 << C.KERNEL_NAMES.index(n) for n in names)
+        C.check(C.lib().cocoa_stats_kernels(self.h, mask), self.h)
+
     def stats_reset(self):
         C.check(C.lib().cocoa_stats_reset(self.h), self.h)
 

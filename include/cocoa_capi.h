@@ -304,6 +304,10 @@ int cocoa_samples(cocoa_ctx *ctx, int32_t part, int32_t seed_plus_t, int32_t cou
 #define COCOA_K_COUNT 8
 /* enable = 1: bracket every launch with HIP events on the context stream. */
 int cocoa_stats_enable(cocoa_ctx *ctx, int enable);
+/* Which kernel ids (bit i = COCOA_K_i) stats bracket when enabled; default all.
+ * Each bracketed launch adds two event packets to its stream, ~5-10 us of
+ * launch-to-launch latency on a short kernel. */
+int cocoa_stats_kernels(cocoa_ctx *ctx, uint32_t mask);
 /* total device milliseconds and launch count per kernel id since last reset */
 int cocoa_kernel_stats(cocoa_ctx *ctx, int kernel, double *total_ms, int64_t *launches);
 int cocoa_stats_reset(cocoa_ctx *ctx);

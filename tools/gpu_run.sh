@@ -95,7 +95,7 @@ for step in "$@"; do
         v=${v//=/_}
         env $envset COCOA_LIB=$lib timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-gap ${BENCH_ARGS} \
           > $O/ab_${v}_$TAG.json 2> $O/ab_${v}_$TAG.err || exit $?
-        python3 -c "import json;d=json.loads(open('$O/ab_${v}_$TAG.json').readlines()[-1]);k=d['kernel_ms'];print('$v', 'step', round(d['ms_per_step'],4), 'solver', round(k['solver'],4), 'gram', round(k['gram'],4), 'eval', round(k['eval'],4), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
+        python3 -c "import json;d=json.loads(open('$O/ab_${v}_$TAG.json').readlines()[-1]);k=d['kernel_ms'];print('$v', 'step', round(d['ms_per_step'],4), 'solver', round(k['solver'],4), 'gram', round(k.get('gram',0),4), 'eval', round(k['eval'],4), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

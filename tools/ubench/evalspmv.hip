@@ -30,7 +30,7 @@ using namespace cocoa;
     } while (0)
 
 namespace cocoa {
-void launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
+bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
 int eval_fast_blocks(int64_t n, int64_t n_test);
 }
 
