@@ -75,7 +75,21 @@ __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_
         const int64_t jo = inv ? inv[j] : j;
         double s = init ? init[jo] + dw[j] : dw[j];
         if (zero) dw[j] = 0.0;
-        for (int32_t k = 1; k < K; ++k) {
+        int32_t k = 1;
+        // eight slices' loads in flight at a time (the zero stores, which may
+        // alias as far as the compiler knows, go after them); partition order kept
+        for (; k + 8 <= K; k += 8) {
+            double v[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] = dw[(size_t)(k + t) * d + j];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) s = s + v[t];
+            if (zero) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) dw[(size_t)(k + t) * d + j] = 0.0;
+            }
+        }
+        for (; k < K; ++k) {
             const size_t o = (size_t)k * d + j;
             s = s + dw[o];
             if (zero) dw[o] = 0.0;
