@@ -1017,6 +1017,8 @@ static void plan_solver(cocoa_ctx* c, int64_t vec_len, bool need_prod = true) {
     // several workgroups per CU: no LDS-resident vector, stream of at least 512
     // entries (a batch still holds a few rows)
     while (want > 1 && cap > 512 && fixed_for(cap) > budget) cap /= 2;
+    if (const char* e = std::getenv("COCOA_CHAIN_CAP"))  // A/B: a smaller stream, more LDS for the hot slice
+        cap = std::max<size_t>(256, std::min<size_t>(cap, (size_t)std::atoi(e)));
     const size_t fixed = fixed_for(cap);
     size_t avail = (want > 1 ? budget : kLdsMax) - std::min(fixed, budget);
     c->vec_lds = is_sdca(c->method) && vec_bytes <= avail && want == 1;
@@ -1042,6 +1044,24 @@ static void plan_solver(cocoa_ctx* c, int64_t vec_len, bool need_prod = true) {
     if (c->alpha_lds) {
         a.lds_alpha = (int32_t)off;
         off += al_bytes;
+    }
+    // fast CoCoA+ on compact slices (C4): the LDS left over holds each slice's
+    // first positions -- the partition's most frequent columns -- so their
+    // gathers and stores stay off HBM lines (COCOA_CHAIN_HOT=0: off, A/B)
+    a.hot = 0;
+    a.lds_hot = 0;
+    const char* he = std::getenv("COCOA_CHAIN_HOT");
+    if (!c->strict && c->dw_compact && c->method == COCOA_METHOD_COCOA_PLUS && !c->vec_lds &&
+        !(he && !std::atoi(he))) {
+        const size_t lim = want > 1 ? budget : kLdsMax;
+        const int64_t h = off < lim ? std::min<int64_t>((int64_t)((lim - off) / sizeof(double)) & ~(int64_t)63,
+                                                        c->max_u)
+                                    : 0;
+        if (h >= 64) {
+            a.hot = (int32_t)h;
+            a.lds_hot = (int32_t)off;
+            off += align16(sizeof(double) * (size_t)h);
+        }
     }
     c->lds_bytes = off;
     a.stream_cap = (int32_t)cap;
@@ -3021,13 +3041,13 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
-                  "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d}",
+                  "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d}",
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,
                   ctx->dw_dbuf ? 1 : 0, ctx->use_dense ? "dense" : ctx->use_gram ? "gram" : "chain",
                   ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u,
                   !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
-                  ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0);
+                  ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot);
     CAPI_END(ctx)
 }

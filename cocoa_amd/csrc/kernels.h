@@ -90,6 +90,11 @@ struct SolverArgs {
     int32_t lds_scratch;      // compute scratch: kRegChunks*64 doubles
     int32_t lds_vec;          // d doubles (deltaW, or w_loc for CoCoA) if VEC_LDS
     int32_t lds_alpha;        // rows-of-largest-partition doubles if ALPHA_LDS
+    // fast CoCoA+ on compact slices: slice positions [0, hot) -- the partition's
+    // most frequent columns (slices list them in device order) -- live in LDS
+    // at lds_hot for the launch, written back to the slice at its end
+    int32_t hot;
+    int32_t lds_hot;
     uint64_t* prof;           // optional cycle counters [K][2 waves][16] (diagnostics)
 };
 

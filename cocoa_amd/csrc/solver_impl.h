@@ -445,10 +445,26 @@ __device__ __forceinline__ void read_chunks3(const int32_t* scol, const double* 
 
 // RC: register chunks per row (rows with z <= 64 * RC take the register path);
 // SolverArgs::reg_chunks picks 3 or 4 from the data's mean row length.
-template <int MODE, bool VEC_LDS, int RC>
+template <int MODE, bool VEC_LDS, int RC, bool HOT = false>
 __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const int32_t* scol, const double* sval,
-                               double* vec, double* alv) {
+                               double* vec, double* alv, double* hl = nullptr) {
     const int lane = lane_id();
+    // HOT: slice positions below a.hot in LDS (hl); a hot lane's global load goes
+    // to position 0 (one line for the wave, never written in HBM by this launch)
+    const int32_t hot = HOT ? a.hot : 0;
+    auto get = [&](int32_t c) -> double {
+        if (!HOT) return vec[c];
+        const bool h = c < hot;
+        const double lv = hl[h ? c : 0];
+        const double gv = vec[h ? 0 : c];
+        return h ? lv : gv;
+    };
+    auto put = [&](int32_t c, double v) {
+        if (HOT && c < hot)
+            hl[c] = v;
+        else
+            vec[c] = v;
+    };
     const int m = uni(mb->m);
     const double lam_n = a.lam_n;
     const double inv_lam_n = 1.0 / a.lam_n;
@@ -486,7 +502,7 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
             // v = 0), then the next step's staged inputs
             double pd[RC];
 #pragma unroll
-            for (int u = 0; u < RC; ++u) pd[u] = vec[ch.c[u]];
+            for (int u = 0; u < RC; ++u) pd[u] = get(ch.c[u]);
             next(s);
             double acc = 0.0;
 #pragma unroll
@@ -496,7 +512,7 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
             if (uni((int32_t)go)) {
 #pragma unroll
                 for (int u = 0; u < RC; ++u)
-                    if (u < nch && lane + 64 * u < st.z) vec[ch.c[u]] = fma(ch.v[u], coef, pd[u]);  // deltaW += update
+                    if (u < nch && lane + 64 * u < st.z) put(ch.c[u], fma(ch.v[u], coef, pd[u]));  // deltaW += update
                 if (lane == 0) alv[st.r] = na;                   // CoCoA.scala:186
             }
             continue;
@@ -518,7 +534,7 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
                     v4[u] = p < st.z ? sv[p] : 0.0;
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) g4[u] = vec[c4[u]];
+                for (int u = 0; u < 4; ++u) g4[u] = get(c4[u]);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) acc = fma(v4[u], g4[u], acc);
             }
@@ -543,7 +559,7 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
                 const double* sv = st.off >= 0 ? sval + st.off : a.val + uni(mb->beg[s]);
                 if (st.fl & 1) {
                     if (lane == 0)
-                        for (int32_t q = 0; q < st.z; ++q) vec[sc[q]] = vec[sc[q]] + sv[q] * coef;
+                        for (int32_t q = 0; q < st.z; ++q) put(sc[q], get(sc[q]) + sv[q] * coef);
                 } else {
                     // distinct columns: a pass's reads all go out before its writes
                     for (int32_t p0 = 0; p0 < st.z; p0 += 256) {
@@ -556,10 +572,10 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
                             v4[u] = p < st.z ? sv[p] : 0.0;
                         }
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) g4[u] = c4[u] >= 0 ? vec[c4[u]] : 0.0;
+                        for (int u = 0; u < 4; ++u) g4[u] = c4[u] >= 0 ? get(c4[u]) : 0.0;
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
-                            if (c4[u] >= 0) vec[c4[u]] = fma(v4[u], coef, g4[u]);
+                            if (c4[u] >= 0) put(c4[u], fma(v4[u], coef, g4[u]));
                     }
                 }
             }
@@ -570,7 +586,7 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
 
 // RC: chain v3 register chunks, a separate instantiation per count (one kernel
 // holding both paths measured slower: its register allocation covers both).
-template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS, int RC = kRegChunks>
+template <int MODE, bool STRICT, bool VEC_LDS, bool ALPHA_LDS, int RC = kRegChunks, bool HOT = false>
 __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int k = blockIdx.x;
@@ -588,6 +604,9 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
     double* alv = ALPHA_LDS ? (double*)(lds + a.lds_alpha) : a.alpha_work + p0;
     double* scratch = (double*)(lds + a.lds_scratch);
     double* prod = (double*)(lds + a.lds_prod);
+    double* hl = HOT ? (double*)(lds + a.lds_hot) : nullptr;
+    if (HOT)
+        for (int32_t j = tid; j < a.hot; j += 128) hl[j] = 0.0;  // (the slice is zero on entry)
 
     // prologue: alphaOld stays in a.alpha; the working copy is alv
     for (int32_t i = tid; i < nl; i += 128) alv[i] = a.alpha[p0 + i];
@@ -613,8 +632,8 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
                                      (int32_t*)(lds + a.lds_stream_col[cur ^ 1]), (double*)(lds + a.lds_stream_val[cur ^ 1]),
                                      prod);
         } else if (!STRICT && MODE != MODE_COCOA) {
-            compute_batch3<MODE, VEC_LDS, RC>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
-                                              (const double*)(lds + a.lds_stream_val[cur]), vec, alv);
+            compute_batch3<MODE, VEC_LDS, RC, HOT>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
+                                                   (const double*)(lds + a.lds_stream_val[cur]), vec, alv, hl);
         } else {
             compute_batch<MODE, STRICT, VEC_LDS, ALPHA_LDS>(a, mb, (const int32_t*)(lds + a.lds_stream_col[cur]),
                                                             (const double*)(lds + a.lds_stream_val[cur]), scratch, vec,
@@ -650,6 +669,8 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
     }
     if (VEC_LDS && MODE != MODE_COCOA)
         for (int64_t j = tid; j < d; j += 128) dwk[j] = vec[j];
+    if (HOT)
+        for (int32_t j = tid; j < a.hot; j += 128) dwk[j] = hl[j];
 }
 
 template <bool STRICT>
@@ -659,6 +680,9 @@ void launch_solver_impl(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
     do {                                                                                             \
         constexpr int RCS = short_row_chunks(M, STRICT);                                           \
         auto kern = a.reg_chunks == RCS ? solver_kernel<M, STRICT, V, A, RCS> : solver_kernel<M, STRICT, V, A>; \
+        if constexpr (M == MODE_PLUS && !STRICT && !V)                                               \
+            if (a.hot > 0) kern = a.reg_chunks == RCS ? solver_kernel<M, STRICT, V, A, RCS, true>       \
+                                                      : solver_kernel<M, STRICT, V, A, kRegChunks, true>; \
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
         kern<<<grid, 128, lds, s>>>(a);                                                              \
     } while (0)

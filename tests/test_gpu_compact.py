@@ -140,3 +140,22 @@ def test_block_fold_matches_gather_fold(solver, monkeypatch):
     assert np.max(np.abs(a.alpha() - b.alpha())) <= 1e-12
     for x, y in zip(ea, eb):
         assert abs(x["gap"] - y["gap"]) <= 1e-12 * abs(y["primal"]) and x["test_err_count"] == y["test_err_count"]
+
+
+def test_chain_hot_slice_positions_in_lds_are_bitwise_neutral(monkeypatch):
+    """Fast CoCoA+ on compact slices keeps each slice's first positions (the
+    partition's most frequent columns) in LDS for the launch (SolverArgs::hot).
+    Where a value lives does not change the solver's arithmetic; the same rounds
+    with COCOA_CHAIN_HOT=0 agree to 1e-12 (the block fold's fp64 atomic adds,
+    where work items share a column block, reassociate between runs)."""
+    sh = configs.share("c4", n=20000, d=300000, parts=16, n_test=1000)
+    a, ea = run(sh, "cocoa+", True, monkeypatch, rounds=3, solver="chain")
+    assert a.plan()["chain_hot"] >= 1024 and a.plan()["vec_lds"] == 0, a.plan()
+    monkeypatch.setenv("COCOA_CHAIN_HOT", "0")
+    b, eb = run(sh, "cocoa+", True, monkeypatch, rounds=3, solver="chain")
+    assert b.plan()["chain_hot"] == 0
+    wb = b.w()
+    assert np.max(np.abs(a.w() - wb)) <= 1e-12 * np.max(np.abs(wb))
+    assert np.max(np.abs(a.alpha() - b.alpha())) <= 1e-12
+    for x, y in zip(ea, eb):
+        assert abs(x["gap"] - y["gap"]) <= 1e-12 * abs(y["primal"]) and x["test_err_count"] == y["test_err_count"]

@@ -352,6 +352,7 @@ def test_c4_one_gpu_k1024_fast_vs_oracle(c4_full):
     assert plan["solver"] == "chain" and plan["dw_compact"] == 1 and plan["fold"] == "blocks", plan
     # four chain workgroups per CU: 1,024 partitions on 256 CUs all resident at once
     assert plan["lds_bytes"] <= 40 * 1024 and plan["stream_cap"] == 1024 and plan["alpha_lds"] == 0, plan
+    assert plan["chain_hot"] >= 512, plan  # the LDS left over: each slice's most frequent columns
     run = make_run(sh, od, "cocoa+")
     for t in (1, 2, 3):
         e.round(t)
