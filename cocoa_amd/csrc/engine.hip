@@ -274,6 +274,8 @@ struct cocoa_ctx {
     // cocoa_eval_end (single rank, one device); other contexts hold the finished
     // result in eval_held
     bool inl_pending = false;
+    bool inl_ranks = false;       //   its sums all-reduced across ranks on the device (fast multi-rank)
+    int64_t n_test_glob = -1;     // test rows over all ranks (-1: not yet exchanged for this test set)
     hipEvent_t e_inl = nullptr;
     cocoa_eval_result eval_held{};
     bool eval_fired = false;    //   and its kernels enqueued on estream
@@ -975,6 +977,7 @@ static void set_test_impl(cocoa_ctx* ctx, bool dense_in, const int64_t* row_ptr,
     ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s, eval_tile_entries());
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
+    ctx->n_test_glob = -1;  // (re-exchanged at the next multi-rank cocoa_eval_begin)
     if (ctx->inited) {
         const size_t rows = (size_t)(ctx->tr.n + ctx->te.n);
         ctx->row_scratch.alloc(sizeof(double) * std::max<size_t>(rows, 1));
@@ -1830,6 +1833,7 @@ extern "C" int cocoa_comm_init(cocoa_ctx* ctx, int transport, int32_t rank, int3
     delete ctx->comm;
     ctx->comm = nullptr;
     ctx->comm = cocoa::comm_create(transport, rank, world, uid, ctx->device);
+    ctx->n_test_glob = -1;
     CAPI_END(ctx)
 }
 
@@ -1870,7 +1874,7 @@ static void finish(const cocoa_ctx* c, double hinge, double alpha_sum, double w2
 // async (cocoa_eval_async): on estream, from the (w, alpha) snapshots, into
 // eval_part2 / eval_out2 and h_eval[4..7]; no row x.w kept (the next round's
 // plan forms x.w itself)
-static void eval_launch(cocoa_ctx* ctx, bool async = false) {
+static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true) {
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     require(async || !ctx->eval_pending, COCOA_E_STATE,
             "an evaluation is pending: collect it with cocoa_eval_wait first");
@@ -1926,7 +1930,7 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false) {
                 DevBuf& cnt = async ? ctx->eval_cnt2 : ctx->eval_cnt;
                 if (!cnt.p) cnt.alloc_zero(sizeof(unsigned), st);
                 e.counter = cnt.as<unsigned>();
-                e.out_host = ctx->h_eval + (async ? 4 : 0);
+                e.out_host = to_host ? ctx->h_eval + (async ? 4 : 0) : nullptr;
                 host_done = launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), st);
             }
             ctx->xw_cached = !async;  // the next round's plan reuses these x.w (stream order)
@@ -1936,7 +1940,7 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false) {
         if (!host_done)
             HIPCHK(hipMemcpyAsync(ctx->h_eval + 4, ctx->eval_out2.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
         HIPCHK(hipEventRecord(ctx->e_done, st));
-    } else if (!host_done) {
+    } else if (!host_done && to_host) {
         HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
     }
 }
@@ -2057,8 +2061,9 @@ static void eval_fire(cocoa_ctx* ctx) {
 
 void cocoa_ctx::eval_quiesce() {
     if (inl_pending) {  // an uncollected cocoa_eval_begin: its result is dropped
-        HIPCHK(hipEventSynchronize(e_inl));
+        if (e_inl) HIPCHK(hipEventSynchronize(e_inl));
         inl_pending = false;
+        inl_ranks = false;
     }
     if (!eval_pending) return;
     eval_fire(this);
@@ -2094,6 +2099,28 @@ extern "C" int cocoa_eval_begin(cocoa_ctx* ctx) {
     require(ctx->inited, COCOA_E_STATE, "call cocoa_init first");
     require(!ctx->inl_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_end first");
     require(!ctx->eval_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_wait first");
+    if (!ctx->is_group() && ctx->comm && ctx->comm->world > 1 && !ctx->strict) {
+        // fast multi-rank: the rank sums all-reduced on the device behind the pass
+        // (hinge and alpha sums, then the error count; ||w||^2 is the same on
+        // every rank), read back by cocoa_eval_end.  Over RCCL nothing here waits
+        // for the GPU; the HOST transport stages through the host as always.
+        cocoa::Comm& cm = *ctx->comm;
+        if (ctx->n_test_glob < 0) {  // (once per test set: every rank takes this branch together)
+            double nt = (double)(ctx->has_test ? ctx->te.n : 0);
+            cm.allreduce(&nt, 1, false, ctx->stream);
+            ctx->n_test_glob = (int64_t)nt;
+        }
+        if (!ctx->e_inl) HIPCHK(hipEventCreateWithFlags(&ctx->e_inl, hipEventDisableTiming));
+        eval_launch(ctx, false, false);
+        double* out = ctx->eval_out.as<double>();
+        cm.allreduce(out, 2, true, ctx->stream);
+        cm.allreduce(out + 3, 1, true, ctx->stream);
+        HIPCHK(hipMemcpyAsync(ctx->h_eval, out, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipEventRecord(ctx->e_inl, ctx->stream));
+        ctx->inl_ranks = true;
+        ctx->inl_pending = true;
+        return COCOA_OK;
+    }
     if (ctx->is_group() || (ctx->comm && ctx->comm->world > 1)) {
         cocoa_eval_result r{};
         const int rc = cocoa_eval(ctx, &r);
@@ -2113,6 +2140,13 @@ extern "C" int cocoa_eval_end(cocoa_ctx* ctx, cocoa_eval_result* out) {
     require(out != nullptr, COCOA_E_ARG, "null out");
     require(ctx->inl_pending, COCOA_E_STATE, "cocoa_eval_end: no evaluation pending (cocoa_eval_begin)");
     ctx->inl_pending = false;
+    if (ctx->inl_ranks) {
+        ctx->inl_ranks = false;
+        HIPCHK(hipEventSynchronize(ctx->e_inl));
+        const double* h = ctx->h_eval;
+        finish(ctx, h[0], h[1], h[2], (int64_t)h[3], ctx->n_test_glob, out);
+        return COCOA_OK;
+    }
     if (ctx->is_group() || (ctx->comm && ctx->comm->world > 1)) {
         *out = ctx->eval_held;
         return COCOA_OK;

@@ -94,10 +94,11 @@ def _rank_worker(rank, world, strict, methods, uid_q, out_q):
         out_q.put((rank, repr(ex)))
 
 
-def _spawn(world, strict, methods):
+def _spawn(world, strict, methods, target=None):
     ctx = mp.get_context("spawn")
     uid_q, out_q = ctx.Queue(), ctx.Queue()
-    procs = [ctx.Process(target=_rank_worker, args=(r, world, strict, methods, uid_q, out_q)) for r in range(world)]
+    target = target or _rank_worker
+    procs = [ctx.Process(target=target, args=(r, world, strict, methods, uid_q, out_q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -144,6 +145,54 @@ def test_multirank_strict_chain_is_bitwise_single_process(world):
     assert out[0]["run"][0].tobytes() == run.w().tobytes()
     assert [t for t, _ in out[0]["run"][1]] == [4, 8]
     assert [ev["gap"].hex() for _, ev in out[0]["run"][1]] == [rv["gap"].hex() for rv in revs]
+
+
+def _defer_worker(rank, world, strict, methods, uid_q, out_q):
+    """Fast CoCoA+ with each evaluation's read-back deferred past the next round
+    (cocoa_eval_begin / _end): the rank sums are all-reduced on the device."""
+    try:
+        tr = cocoa_amd.load_libsvm(TRAIN, 4, 9947)
+        te = cocoa_amd.load_libsvm(TEST, 4, 9947)
+        k0, k1 = shard_bounds(4, world, rank)
+        r0, r1 = shard_bounds(te.n, world, rank)
+        if rank == 0:
+            uid = comm_unique_id("host")
+            for _ in range(world - 1):
+                uid_q.put(uid)
+        else:
+            uid = uid_q.get(timeout=60)
+        e = Engine(device=0, strict=False)
+        e.set_train(tr.shard(k0, k1), part_begin=k0, num_parts_global=4)
+        e.set_test(te.row_range(r0, r1))
+        e.comm_init("host", rank, world, uid)
+        e.init("cocoa+", tr.n, T + 1, H, LAM, 1.0, 1.0, 4, 0)
+        evs, pending = [], False
+        for t in range(1, T + 2):
+            e.round(t)  # (round t+1 is enqueued before round t's evaluation is read back)
+            if pending:
+                evs.append(e.eval_end())
+                pending = False
+            if t % 4 == 0 and t <= T:
+                e.eval_begin()
+                pending = True
+        out_q.put((rank, evs))
+    except Exception as ex:
+        out_q.put((rank, repr(ex)))
+
+
+def test_multirank_fast_deferred_eval_device_allreduce():
+    """cocoa_eval_begin on a fast multi-rank context all-reduces the objective
+    sums on the device and cocoa_eval_end reads them back: the oracle's values
+    within 1e-9, the same bytes on every rank, the global test-row count."""
+    world = 2
+    out = _spawn(world, False, None, target=_defer_worker)
+    _, revs = _oracle("cocoa+")
+    assert len(out[0]) == len(revs) == T // 4
+    for a, b, rv in zip(out[0], out[1], revs):
+        assert a["gap"].hex() == b["gap"].hex() and a["primal"].hex() == b["primal"].hex()
+        assert abs(a["primal"] - rv["primal"]) <= 1e-9 * abs(rv["primal"])
+        assert abs(a["gap"] - rv["gap"]) <= 1e-9 * abs(rv["primal"])
+        assert a["test_err_count"] == rv["test_err"] and a["test_rows"] == 600
 
 
 def test_multirank_fast_allreduce_within_tolerance():
