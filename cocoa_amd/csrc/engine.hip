@@ -227,6 +227,7 @@ struct cocoa_ctx {
     DevBuf w, alpha, alpha_work, dw, wloc, samples, dw_sum_int, eval_part, eval_out, row_scratch, jump, prof;
     double* dw_sum = nullptr;
     bool dw_sum_user = false;  // dw_sum is the caller's buffer (cocoa_set_dw_sum_buffer), else dw_sum_int
+    bool abort_in_sum = false; // dw_sum[d] holds the all-reduced abort flag of the last exchange
     double* h_eval = nullptr;  // pinned [4]
     int64_t samples_cap = 0;
 
@@ -467,6 +468,14 @@ static void make_side_stream(hipStream_t* st, int reserve, int ncu, int prio) {
 
 static void check_status(cocoa_ctx* c) {
     if (!c->use_gram || !c->status.p) return;
+    if (c->abort_in_sum) {  // the all-reduced abort slot of the last exchange (cocoa_round)
+        double sl = 0.0;
+        HIPCHK(hipMemcpyAsync(&sl, c->dw_sum + c->d, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (sl != 0.0)
+            throw Error(COCOA_E_HIP, "local solver: a hand-off between the solver's waves timed out on some rank "
+                                     "(launch aborted)");
+    }
     int st = 0;
     // on the context's stream (the solver's), not the null stream, which would
     // also wait for the CU-masked side streams (created blocking)
@@ -518,7 +527,7 @@ extern "C" int cocoa_create(int device, int strict, void* stream, cocoa_ctx** ou
             HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
             c->own_stream = true;
         }
-        HIPCHK(hipHostMalloc((void**)&c->h_eval, 8 * sizeof(double), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&c->h_eval, 16 * sizeof(double), hipHostMallocDefault));
         // jump table (A_j, C_j), j = 1..256, for the sampler
         std::vector<uint64_t> jt(512);
         for (int j = 1; j <= 256; ++j) jr_jump((uint64_t)j, &jt[2 * (j - 1)], &jt[2 * (j - 1) + 1]);
@@ -1183,7 +1192,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         ctx->wloc.free();
     ctx->samples_cap = std::max<int64_t>((int64_t)K * H, 1);
     ctx->samples.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
-    ctx->dw_sum_int.alloc(sizeof(double) * (size_t)d);
+    ctx->dw_sum_int.alloc(sizeof(double) * ((size_t)d + 1));  // (+1: the abort slot of a multi-rank exchange)
+    ctx->abort_in_sum = false;
     // (re-allocated on every init: a pointer kept from an earlier init would dangle)
     if (!ctx->dw_sum_user) ctx->dw_sum = ctx->dw_sum_int.as<double>();
     ctx->eval_part.alloc(sizeof(double) * (size_t)std::max<int64_t>(4 * 2048, 2 * K + 8));
@@ -1744,6 +1754,14 @@ extern "C" int cocoa_round(cocoa_ctx* ctx, int32_t t) {
             run_local(ctx, t, false, cm.rank > 0 ? ctx->dw_sum : nullptr);
             cm.chain_send(ctx->dw_sum, d, true, ctx->stream);
             cm.bcast_last(ctx->dw_sum, d, true, ctx->stream);
+        } else if (ctx->use_gram && cm.world > 1 && !ctx->dw_sum_user) {
+            // no host wait: the status word rides along with the sum (slot d), so
+            // every rank sees an abort on any rank at its next synchronising call
+            // (check_status), before it returns any result
+            run_local(ctx, t, false);
+            launch_status_slot(ctx->status.as<int>(), ctx->dw_sum + d, ctx->stream);
+            cm.allreduce(ctx->dw_sum, d + 1, true, ctx->stream);
+            ctx->abort_in_sum = true;
         } else {
             run_local(ctx, t, false);
             checked();
@@ -2116,6 +2134,9 @@ extern "C" int cocoa_eval_begin(cocoa_ctx* ctx) {
         cm.allreduce(out, 2, true, ctx->stream);
         cm.allreduce(out + 3, 1, true, ctx->stream);
         HIPCHK(hipMemcpyAsync(ctx->h_eval, out, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        if (ctx->abort_in_sum)  // the last exchange's all-reduced abort flag, read with the sums
+            HIPCHK(hipMemcpyAsync(ctx->h_eval + 8, ctx->dw_sum + ctx->d, sizeof(double), hipMemcpyDeviceToHost,
+                                  ctx->stream));
         HIPCHK(hipEventRecord(ctx->e_inl, ctx->stream));
         ctx->inl_ranks = true;
         ctx->inl_pending = true;
@@ -2144,6 +2165,9 @@ extern "C" int cocoa_eval_end(cocoa_ctx* ctx, cocoa_eval_result* out) {
         ctx->inl_ranks = false;
         HIPCHK(hipEventSynchronize(ctx->e_inl));
         const double* h = ctx->h_eval;
+        if (ctx->abort_in_sum && h[8] != 0.0)
+            throw Error(COCOA_E_HIP, "local solver: a hand-off between the solver's waves timed out on some rank "
+                                     "(launch aborted)");
         finish(ctx, h[0], h[1], h[2], (int64_t)h[3], ctx->n_test_glob, out);
         return COCOA_OK;
     }

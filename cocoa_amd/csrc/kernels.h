@@ -300,6 +300,8 @@ void launch_fold_compact(double* dw, const int64_t* fptr, const uint32_t* fpos, 
                          double mult, bool apply, const int32_t* inv, bool zero, hipStream_t s,
                          const double* init = nullptr);
 void launch_apply(double* w, const double* dw_sum, int64_t d, double mult, const int32_t* inv, hipStream_t s);
+// *slot = (status[0] != 0): a solver abort rides along with the deltaW all-reduce
+void launch_status_slot(const int* status, double* slot, hipStream_t s);
 void launch_scale(double* w, int64_t d, double scale, hipStream_t s);
 void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, double* out, hipStream_t s);
 void launch_sgd(bool local, const SolverArgs& a, double lambda, double t0, int grid, hipStream_t s);

@@ -101,6 +101,10 @@ __global__ __launch_bounds__(256) void fold_kernel(double* dw, int32_t K, int64_
     }
 }
 
+__global__ void status_slot_kernel(const int* status, double* slot) { *slot = status[0] != 0 ? 1.0 : 0.0; }
+
+void launch_status_slot(const int* status, double* slot, hipStream_t s) { status_slot_kernel<<<1, 1, 0, s>>>(status, slot); }
+
 void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double* w, double mult, bool apply,
                  const int32_t* inv, bool zero, hipStream_t s, const double* init) {
     int blocks = (int)std::min<int64_t>((d + 255) / 256, 2048);
