@@ -1711,6 +1711,7 @@ extern "C" int cocoa_set_dw_sum_buffer(cocoa_ctx* ctx, void* device_ptr) {
     GROUP_REJECT(ctx, "cocoa_set_dw_sum_buffer");
     ctx->dw_sum = device_ptr ? (double*)device_ptr : ctx->dw_sum_int.as<double>();
     ctx->dw_sum_user = device_ptr != nullptr;
+    ctx->abort_in_sum = false;  // (a caller's buffer has no abort slot)
     CAPI_END(ctx)
 }
 
