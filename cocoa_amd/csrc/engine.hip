@@ -2013,7 +2013,7 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
     eval_launch(ctx);
     const EvalLocal ev = eval_collect(ctx);
     double hinge = ev.hinge, alpha_sum = ev.alpha_sum;
-    const double w2 = ev.w2;
+    double w2 = ev.w2;
     double counts[2] = {ev.err, ev.n_test};
     if (ctx->comm && ctx->comm->world > 1) {
         cocoa::Comm& cm = *ctx->comm;
@@ -2026,10 +2026,13 @@ extern "C" int cocoa_eval(cocoa_ctx* ctx, cocoa_eval_result* out) {
             hinge = carry[0];
             alpha_sum = carry[2];
         } else {
-            double sums[2] = {hinge, alpha_sum};
-            cm.allreduce(sums, 2, false, ctx->stream);
+            // ||w||^2: rank 0's on every rank (each rank's pass sums the replicated w
+            // over its own grid, so the last bit may differ between ranks)
+            double sums[3] = {hinge, alpha_sum, cm.rank == 0 ? w2 : 0.0};
+            cm.allreduce(sums, 3, false, ctx->stream);
             hinge = sums[0];
             alpha_sum = sums[1];
+            w2 = sums[2];
         }
         cm.allreduce(counts, 2, false, ctx->stream);  // integers: exact in any order
     }
@@ -2132,7 +2135,9 @@ extern "C" int cocoa_eval_begin(cocoa_ctx* ctx) {
         if (!ctx->e_inl) HIPCHK(hipEventCreateWithFlags(&ctx->e_inl, hipEventDisableTiming));
         eval_launch(ctx, false, false);
         double* out = ctx->eval_out.as<double>();
-        cm.allreduce(out, 2, true, ctx->stream);
+        // ||w||^2: rank 0's everywhere (each rank sums the replicated w over its own grid)
+        if (cm.rank != 0) HIPCHK(hipMemsetAsync(out + 2, 0, sizeof(double), ctx->stream));
+        cm.allreduce(out, 3, true, ctx->stream);
         cm.allreduce(out + 3, 1, true, ctx->stream);
         HIPCHK(hipMemcpyAsync(ctx->h_eval, out, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
         if (ctx->abort_in_sum)  // the last exchange's all-reduced abort flag, read with the sums
