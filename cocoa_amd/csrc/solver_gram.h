@@ -146,26 +146,17 @@ __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F
 //     XP[p][c] of the partners; G_hot = XP[0..15] XP^T with lanes =
 //     partners and the updater values broadcast from LDS;
 //   cold columns: an LDS hash (column -> list of (updater, value)) of the
-//     updaters' cold entries, filled tile by tile (kGramTile packed positions
-//     of the updater rows at a time); every partner cold entry probes it.
+//     updaters' cold entries, filled tile by tile; every partner cold entry
+//     probes it.  A tile holds the updaters' COLD entries only, numbered in
+//     position order (a block-wide ballot scan), so 1,024 cover a typical
+//     batch (16 rows x ~76 entries, ~2/3 cold) and the LDS fits three
+//     workgroups per CU (round 4; tiles of 2,048 packed positions, two per CU,
+//     took 2.25 ms against 2.20).
 // Windows longer than the register chunk reload it per tile (same results).
-#ifndef COCOA_GRAM_V2
-#define COCOA_GRAM_V2 1
-#endif
-#if COCOA_GRAM_V2
-// hash tiles hold the updaters' COLD entries only, numbered in position order
-// (a block-wide ballot scan), so a tile of 1,024 covers a typical batch
-// (16 rows x ~76 entries, ~2/3 cold) and the LDS fits three workgroups per CU
 constexpr int kGramTable = 2048;     // hash slots (power of two, 2 x kGramTile)
 constexpr int kGramTile = 1024;      // cold updater entries per hash tile
 constexpr int kGramNU = 8;           // kGramThreads-entry units in registers
 constexpr int kGramWGs = 3;          // workgroups per CU (LDS, and <= 80 VGPRs)
-#else
-constexpr int kGramTable = 4096;     // hash slots (power of two, 2 x kGramTile)
-constexpr int kGramTile = 2048;      // updater positions per hash tile (16 rows of ~128 entries: one tile)
-constexpr int kGramNU = 12;          // kGramThreads-entry units in registers
-constexpr int kGramWGs = 2;          // workgroups per CU (LDS)
-#endif
 constexpr int kGramThreads = 512;    // 8 waves
 constexpr int kGramCH = kGramNU * kGramThreads;
 constexpr int kGHotS = kGHot + 1;    // XP row stride (doubles)
@@ -180,13 +171,11 @@ struct GramLds {
     int8_t eu[kGramTile];
     int64_t pbeg[kGSlots];
     int32_t pcum[kGSlots + 1];       // packed offsets of the partners
-#if COCOA_GRAM_V2
     int32_t cpre[kGramNU * (kGramThreads / 64)];  // cold-entry rank of each (unit, wave) in a chunk
     int32_t ctot;                                 // cold entries of the chunk
-#endif
 };
 static_assert(sizeof(GramLds) * kGramWGs <= 160 * 1024, "gram_kernel LDS: kGramWGs workgroups per CU");
-static_assert(!COCOA_GRAM_V2 || kGramNU * (kGramThreads / 64) == 64, "one lane per (unit, wave) in the rank scan");
+static_assert(kGramNU * (kGramThreads / 64) == 64, "one lane per (unit, wave) in the rank scan");
 static_assert(kGramThreads == 512, "gram_kernel's hot part gives each of the 8 waves two updaters");
 static_assert(kGramNU % 4 == 0, "gram_kernel probes four units at a time");
 
@@ -298,7 +287,6 @@ __global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a
         }
         L.enext[i] = (int16_t)atomicExch(&L.thead[h], i);
     };
-#if COCOA_GRAM_V2
     // cold part, one hash tile of cold updater entries at a time: entry rank =
     // cold updater entries before it in position order (q = qa + 512 u + tid:
     // unit, wave, lane), the same in every tile's pass
@@ -338,24 +326,6 @@ __global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a
             __syncthreads();  // cpre / ctot of the next chunk
         }
         ncold = run;
-#else
-    // cold part, one hash tile of updater positions at a time
-    for (int32_t ta = 0; ta < Q16; ta += kGramTile) {
-        for (int i = tid; i < kGramTable; i += kGramThreads) {
-            L.tkey[i] = -1;
-            L.thead[i] = -1;
-        }
-        __syncthreads();
-        const int32_t tb = min(Q16, ta + kGramTile);
-        for (int32_t qa = (ta / kGramCH) * kGramCH; qa < tb; qa += kGramCH) {
-            load(qa);
-#pragma unroll
-            for (int u = 0; u < kGramNU; ++u) {
-                const int32_t q = qa + u * kGramThreads + tid;
-                if (q >= ta && q < tb && cc[u] >= kGHot) insert(q - ta, u);
-            }
-        }
-#endif
         __syncthreads();
         phase(5);
         // entries of updater rows of column c from i on (list order), into partner pp
@@ -423,9 +393,7 @@ __global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a
         }
         __syncthreads();
         phase(6);
-#if COCOA_GRAM_V2
         if (ta + kGramTile >= ncold) break;
-#endif
     }
     phase(2);
     // hot part: wave wv -> updaters 2 wv, 2 wv + 1, lane = partner
