@@ -13,12 +13,18 @@ Scaling (cocoa_amd.configs): weak by default -- every GPU holds its own
 globally, H unchanged); --scaling strong keeps one fixed problem (n, K) and
 splits its partitions over the GPUs (C3: K = 64 on 1-8 GPUs; C4: K = 1,024).
 
-Prints one JSON line (rank 0).  Launch N > 1 with
+Prints one JSON line (rank 0).  N > 1 ranks, one process per GPU, either way:
+  python bench.py --gpus N      (this process spawns the N ranks itself, before
+                                 any GPU call, and relays rank 0's line)
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+A rank whose WORLD_SIZE differs from --gpus fails.
 """
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -72,7 +78,62 @@ def eval_bytes(tr, te, d, dense):
             + 12 * te.nnz + 8 * (te.n + 1) + 8 * te.n)
 
 
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, timeout_s=None):
+    """Launch n ranks of this script (one process per GPU, CoCoA.scala:45-48's
+    partition blocks), each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    and relay rank 0's stdout.  Runs in a parent that has made no GPU call (no
+    torch.cuda, no Engine), so the children own the devices.  Returns the worst
+    child exit status; once one rank fails the others get 30 s to end (they
+    would wait at a barrier forever) and are then killed by PID."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, cwd=ROOT,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=r == 0))
+    chunks = []
+    import threading
+    drain = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    drain.start()
+    t0 = time.time()
+    first_fail = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad and first_fail is None:
+            first_fail = time.time()
+        late = (first_fail is not None and time.time() - first_fail > 30) or \
+               (timeout_s is not None and time.time() - t0 > timeout_s)
+        if late:
+            for p in procs:
+                if p.poll() is None:
+                    log(f"killing rank pid {p.pid}")
+                    p.send_signal(signal.SIGKILL)
+        time.sleep(0.2)
+    drain.join(timeout=10)
+    sys.stdout.write("".join(chunks))
+    sys.stdout.flush()
+    rcs = [p.returncode for p in procs]
+    log(f"ranks exited with {rcs}")
+    return max((abs(rc) for rc in rcs), default=0) if any(rcs) else 0
+
+
 def main():
+    if "RANK" not in os.environ and "WORLD_SIZE" not in os.environ:
+        ap0 = argparse.ArgumentParser(add_help=False)
+        ap0.add_argument("--gpus", type=int, default=1)
+        a0, _ = ap0.parse_known_args()
+        if a0.gpus > 1:
+            sys.exit(spawn_ranks(a0.gpus, sys.argv[1:]))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
@@ -110,6 +171,8 @@ def main():
                     help="evaluate each round beside the next one (cocoa_eval_async, the next round's x.w from "
                          "xw_produce_kernel) instead of in line; measured slower on C2 (3.01-3.04 vs 2.90 ms: "
                          "the side work then outgrows the solver)")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="launcher check (no GPU): rank 0 prints {rank, world, master} and every rank exits")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     for k in ("n", "d", "nnz", "parts", "lam", "n_test"):
@@ -122,6 +185,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch N ranks as "
+                         f"'bench.py --gpus N' (spawns them) or torch.distributed.run --nproc-per-node N")
+    if args.launch_probe:
+        if rank == 0:
+            print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank,
+                              "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}))
+        return
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -152,6 +223,9 @@ def main():
     eng.set_test(te)
     eng.init(args.method, n_glob, 1 << 30, H, args.lam)
     runner = DistributedCoCoA(eng, transport=args.transport)
+    comm = eng.comm_info()  # cocoa_comm_info: the exchange the library itself runs
+    if world > 1 and (comm["world"] != world or comm["rank"] != rank):
+        raise SystemExit(f"bench.py: rank {rank}/{world} but the library's communicator says {comm}")
 
     def barrier():
         eng.sync()  # the engine's own HIP stream
@@ -392,6 +466,7 @@ def main():
             "kernel_ms": {k: (v["total_ms"] / v["launches"]) for k, v in stats.items() if v["launches"] > 0},
             "cpu_baseline": cpu,
             "plan": plan,
+            "comm": {"transport": comm["transport"] if world > 1 else None, "world": comm["world"] if world > 1 else 1},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

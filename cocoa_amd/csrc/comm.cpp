@@ -287,7 +287,14 @@ void Comm::host_recv(int fd, void* p, size_t bytes) {
     char* b = (char*)p;
     while (bytes) {
         const ssize_t k = recv(fd, b, bytes, 0);
-        if (k <= 0) throw Error(COCOA_E_IO, std::string("rank exchange recv: ") + (k == 0 ? "peer closed" : std::strerror(errno)));
+        if (k <= 0) {
+            const bool to = k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK);
+            throw Error(COCOA_E_IO, std::string("rank exchange recv: ") +
+                                        (k == 0 ? "peer closed"
+                                         : to ? "timed out waiting for another rank (COCOA_COMM_EXCHANGE_TIMEOUT_MS, "
+                                                "default 1800000 = 30 min, 0 = no limit, raises it)"
+                                              : std::strerror(errno)));
+        }
         b += k;
         bytes -= (size_t)k;
     }

@@ -228,6 +228,9 @@ struct cocoa_ctx {
     double* dw_sum = nullptr;
     bool dw_sum_user = false;  // dw_sum is the caller's buffer (cocoa_set_dw_sum_buffer), else dw_sum_int
     bool abort_in_sum = false; // dw_sum[d] holds the all-reduced abort flag of the last exchange
+    // the solver's status word copied behind an evaluation into pinned memory:
+    // [0] in-line pass (h_eval[9], cocoa_eval_end), [1] pipelined (h_eval[10], cocoa_eval_wait)
+    bool status_slot[2] = {false, false};
     double* h_eval = nullptr;  // pinned [4]
     int64_t samples_cap = 0;
 
@@ -376,9 +379,9 @@ struct cocoa_ctx {
         if (estream) {
             (void)hipStreamSynchronize(estream);
             (void)hipStreamDestroy(estream);
-            (void)hipEventDestroy(e_round);
-            (void)hipEventDestroy(e_done);
         }
+        if (e_round) (void)hipEventDestroy(e_round);
+        if (e_done) (void)hipEventDestroy(e_done);
         if (e_inl) {
             (void)hipEventDestroy(e_inl);
         }
@@ -467,7 +470,8 @@ static void make_side_stream(hipStream_t* st, int reserve, int ncu, int prio) {
 }
 
 static void check_status(cocoa_ctx* c) {
-    if (!c->use_gram || !c->status.p) return;
+    // (the abort slot first: a rank whose own solver is not the Gram one still
+    // receives the all-reduced flag of a rank whose solver aborted)
     if (c->abort_in_sum) {  // the all-reduced abort slot of the last exchange (cocoa_round)
         double sl = 0.0;
         HIPCHK(hipMemcpyAsync(&sl, c->dw_sum + c->d, sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -476,6 +480,7 @@ static void check_status(cocoa_ctx* c) {
             throw Error(COCOA_E_HIP, "local solver: a hand-off between the solver's waves timed out on some rank "
                                      "(launch aborted)");
     }
+    if (!c->use_gram || !c->status.p) return;
     int st = 0;
     // on the context's stream (the solver's), not the null stream, which would
     // also wait for the CU-masked side streams (created blocking)
@@ -1270,10 +1275,15 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                 ctx->gt2.alloc(gtb);
                 ctx->samples2.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
                 const int res = side_reserve(ctx, ncu);
-                if (ctx->gstream && res != ctx->side_res) {  // another CU reservation: a new stream
+                if (ctx->gstream && res != ctx->side_res) {  // another CU reservation: new side streams
                     HIPCHK(hipStreamSynchronize(ctx->gstream));
                     HIPCHK(hipStreamDestroy(ctx->gstream));
                     ctx->gstream = nullptr;
+                    if (ctx->estream) {  // (re-made with the new mask by the next cocoa_eval_async)
+                        HIPCHK(hipStreamSynchronize(ctx->estream));
+                        HIPCHK(hipStreamDestroy(ctx->estream));
+                        ctx->estream = nullptr;
+                    }
                 }
                 ctx->side_res = res;
                 if (!ctx->gstream) {
@@ -1600,6 +1610,14 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.t0 = lsgd_t0;
             const int mode = c->method == COCOA_METHOD_LOCALSGD ? MODE_LSGD : solver_mode(c->method);
             c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(mode, g, K, s); });
+            // fault injection for the abort-reporting tests: COCOA_INJECT_ABORT=t
+            // marks round t's launch as aborted (the status word a timed-out
+            // hand-off sets), on the stream behind it
+            static const int inject_t = std::getenv("COCOA_INJECT_ABORT") ? std::atoi(std::getenv("COCOA_INJECT_ABORT")) : 0;
+            if (inject_t > 0 && t == inject_t) {
+                static const int one = 1;
+                HIPCHK(hipMemcpyAsync(c->status.p, &one, sizeof(int), hipMemcpyHostToDevice, s));
+            }
             if (overlap) {
                 // round t+1's samples and Gram rows on gstream, beside this solver (its
                 // buffer's last reader, round t-1's solver, is done first)
@@ -1755,12 +1773,17 @@ extern "C" int cocoa_round(cocoa_ctx* ctx, int32_t t) {
             run_local(ctx, t, false, cm.rank > 0 ? ctx->dw_sum : nullptr);
             cm.chain_send(ctx->dw_sum, d, true, ctx->stream);
             cm.bcast_last(ctx->dw_sum, d, true, ctx->stream);
-        } else if (ctx->use_gram && cm.world > 1 && !ctx->dw_sum_user) {
+        } else if (cm.world > 1 && !ctx->dw_sum_user) {
             // no host wait: the status word rides along with the sum (slot d), so
             // every rank sees an abort on any rank at its next synchronising call
-            // (check_status), before it returns any result
+            // (check_status), before it returns any result.  Every fast rank sends
+            // d + 1 values whichever solver its own shard took (a rank without the
+            // Gram solver sends 0): RCCL needs the same count on every rank.
             run_local(ctx, t, false);
-            launch_status_slot(ctx->status.as<int>(), ctx->dw_sum + d, ctx->stream);
+            if (ctx->use_gram && ctx->status.p)
+                launch_status_slot(ctx->status.as<int>(), ctx->dw_sum + d, ctx->stream);
+            else
+                HIPCHK(hipMemsetAsync(ctx->dw_sum + d, 0, sizeof(double), ctx->stream));
             cm.allreduce(ctx->dw_sum, d + 1, true, ctx->stream);
             ctx->abort_in_sum = true;
         } else {
@@ -1910,6 +1933,9 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
     if (async) HIPCHK(hipStreamWaitEvent(st, ctx->e_round, 0));  // the snapshots are taken
     if (async && ctx->e_w_rec) HIPCHK(hipStreamWaitEvent(st, ctx->e_w, 0));  // behind this round's plan
     bool host_done = false;  // the sums already stored to h_eval by the pass
+    // the Gram solver's status word rides behind the pass (cocoa_eval_end /
+    // cocoa_eval_wait raise on an aborted launch without a stream sync)
+    const bool gram_status = !ctx->strict && ctx->use_gram && ctx->status.p;
     EvalArgs e{};
     e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     e.col = ctx->tr.col.as<int32_t>();
@@ -1950,11 +1976,18 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
                 if (!cnt.p) cnt.alloc_zero(sizeof(unsigned), st);
                 e.counter = cnt.as<unsigned>();
                 e.out_host = to_host ? ctx->h_eval + (async ? 4 : 0) : nullptr;
+                if (to_host && gram_status) {
+                    e.status = ctx->status.as<int>();
+                    e.status_host = (int*)(ctx->h_eval + (async ? 10 : 9));
+                }
                 host_done = launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), st);
             }
             ctx->xw_cached = !async;  // the next round's plan reuses these x.w (stream order)
         }
     });
+    if (to_host && gram_status && !host_done)
+        HIPCHK(hipMemcpyAsync(ctx->h_eval + (async ? 10 : 9), ctx->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    ctx->status_slot[async ? 1 : 0] = to_host && gram_status;
     if (async) {
         if (!host_done)
             HIPCHK(hipMemcpyAsync(ctx->h_eval + 4, ctx->eval_out2.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1962,6 +1995,15 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
     } else if (!host_done && to_host) {
         HIPCHK(hipMemcpyAsync(ctx->h_eval, ctx->eval_out.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
     }
+}
+
+// the status word an evaluation carried back (eval_launch): raise on an aborted
+// solver launch among the rounds it evaluated
+static void check_status_slot(cocoa_ctx* ctx, int which) {
+    if (!ctx->status_slot[which]) return;
+    ctx->status_slot[which] = false;
+    if (*(volatile int*)(ctx->h_eval + 9 + which) != 0)
+        throw Error(COCOA_E_HIP, "local solver: a hand-off between the solver's waves timed out (launch aborted)");
 }
 
 struct EvalLocal {
@@ -2052,8 +2094,8 @@ extern "C" int cocoa_eval_async(cocoa_ctx* ctx) {
     require(!ctx->inl_pending, COCOA_E_STATE, "an evaluation is pending: collect it with cocoa_eval_end first");
     if (!ctx->estream) {
         make_side_stream(&ctx->estream, ctx->side_res, ctx->ncu, 0);
-        HIPCHK(hipEventCreateWithFlags(&ctx->e_round, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&ctx->e_done, hipEventDisableTiming));
+        if (!ctx->e_round) HIPCHK(hipEventCreateWithFlags(&ctx->e_round, hipEventDisableTiming));
+        if (!ctx->e_done) HIPCHK(hipEventCreateWithFlags(&ctx->e_done, hipEventDisableTiming));
     }
     const size_t nw = sizeof(double) * (size_t)ctx->d, na = sizeof(double) * (size_t)std::max<int64_t>(ctx->tr.n, 1);
     if (ctx->w_snap.bytes < nw) ctx->w_snap.alloc(nw);
@@ -2101,9 +2143,10 @@ extern "C" int cocoa_eval_wait(cocoa_ctx* ctx, cocoa_eval_result* out) {
     eval_fire(ctx);  // no round was issued after cocoa_eval_async
     HIPCHK(hipEventSynchronize(ctx->e_done));
     ctx->eval_pending = false;
-    // no check_status here: the next round's solver (enqueued before this
-    // evaluation fired) may still run on ctx->stream, so its status word is
-    // read by the next call that synchronises that stream (cocoa_sync / cocoa_eval)
+    // the evaluated rounds' status word came back with the sums (h_eval[10]);
+    // the next round's solver, still running, is checked by the next call that
+    // synchronises ctx->stream or collects an evaluation behind it
+    check_status_slot(ctx, 1);
     const double* h = ctx->h_eval + 4;
     finish(ctx, h[0], h[1], h[2], (int64_t)h[3], (int64_t)(ctx->has_test ? ctx->te.n : 0), out);
     CAPI_END(ctx)
@@ -2182,8 +2225,9 @@ extern "C" int cocoa_eval_end(cocoa_ctx* ctx, cocoa_eval_result* out) {
         return COCOA_OK;
     }
     HIPCHK(hipEventSynchronize(ctx->e_inl));
-    // (no check_status: a round enqueued since may still run; the next
-    // synchronising call reads the solver's status word)
+    // the evaluated rounds' status word came back with the sums (h_eval[9]); a
+    // round enqueued since may still run (checked at the next collection or sync)
+    check_status_slot(ctx, 0);
     const double* h = ctx->h_eval;
     finish(ctx, h[0], h[1], h[2], (int64_t)h[3], (int64_t)(ctx->has_test ? ctx->te.n : 0), out);
     CAPI_END(ctx)

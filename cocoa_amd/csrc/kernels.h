@@ -248,6 +248,10 @@ struct EvalArgs {
     // also stores the 4 sums to out_host (pinned) when set
     unsigned* counter;
     double* out_host;
+    // with out_host: the Gram solver's status word (read after the rounds this
+    // pass evaluates, stream order) copied to status_host (pinned), or null
+    const int* status;
+    int* status_host;
 };
 
 // fast translation unit

@@ -371,6 +371,8 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     __shared__ double red4[4][4];
     eval_reduce(a.partials, (int)gridDim.x, a.out, a.out_host, red4, true);
     if (tid == 0) __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    if (tid == 4 && a.status_host)
+        __hip_atomic_store(a.status_host, a.status[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #ifdef COCOA_DIAG

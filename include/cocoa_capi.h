@@ -105,11 +105,17 @@ int cocoa_create(int device, int strict, void *stream, cocoa_ctx **out);
  * holds the contiguous partition block [K r / n, K (r+1) / n) of
  * cocoa_set_train's data (which must be the whole problem: part_begin 0,
  * num_parts_global = num_parts) and the test rows [n_t r / n, n_t (r+1) / n).
- * Every round the devices exchange deltaW on their own streams (peer copies over
- * xGMI; fast: a reduce-scatter then all-gather of column slices, device r
- * summing slice r of every device's fold in device order, so the result is
- * reproducible and identical on every device; strict: the partition-order
- * chain, so strict results stay bitwise equal to one device); cocoa_eval merges the
+ * Every round the devices exchange deltaW on their own streams.  Fast mode,
+ * distinct devices (the default): one grouped RCCL all-reduce over xGMI
+ * (ncclCommInitAll; identical bytes on every device, but the association of
+ * the sum follows RCCL's algorithm and channel choice, so it is not
+ * reproducible across device counts or RCCL versions).  Fast mode with a
+ * repeated ordinal, COCOA_GROUP_EXCHANGE=peer, or an RCCL set-up failure: peer
+ * copies, a reduce-scatter then all-gather of column slices, device r summing
+ * slice r of every device's fold in device order (reproducible and identical
+ * on every device).  cocoa_plan_info reports which ("exchange").  Strict: the
+ * partition-order chain, so strict results stay bitwise equal to one device.
+ * cocoa_eval merges the
  * objective terms; w / alpha / checkpoints are those of the whole problem (a
  * checkpoint is interchangeable with a one-device context's).  The
  * caller-driven exchange entry points (cocoa_round_local, cocoa_round_apply,
