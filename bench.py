@@ -320,6 +320,7 @@ def main():
     ttg = None
     rounds_to_gap = None
     final_gap = None
+    gap_run_s = None
     if not args.no_gap:
         eng.init(args.method, n_glob, 1 << 30, H, args.lam)
         barrier()
@@ -333,6 +334,9 @@ def main():
         final_gap = vals[-1]
         rounds_to_gap = rounds[-1] if final_gap <= args.gap_target else None
         log(f"gap {final_gap:.3g} after {rounds[-1]} rounds, {ttg:.3f}s")
+        gap_run_s = ttg
+        if rounds_to_gap is None:  # the target was not reached: no time-to-gap (gap_run_s says how long it ran)
+            ttg = None
 
     # ---- roofline of the dominant kernel (solver) and of the eval pass -----
     plan = eng.plan()
@@ -450,6 +454,7 @@ def main():
                                       f"{'all-reduce' if not args.strict else 'ordered chain'} inside libcocoa_hip.so "
                                       f"({args.transport.upper()})"},
             "time_to_gap_s": ttg, "rounds_to_gap": rounds_to_gap, "gap_target": args.gap_target,
+            "gap_run_s": gap_run_s, "gap_max_rounds": args.gap_max_rounds,
             "final_gap": final_gap, "gap_trajectory_timed": gaps,
             "roofline": {"kernel": "solver (local SDCA, CoCoA.localSDCA)", "bound": "hbm", "achieved": ach,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": traffic,

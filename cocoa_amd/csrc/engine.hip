@@ -244,11 +244,17 @@ struct cocoa_ctx {
     bool use_gram = false;
     bool use_dense = false;  // dense-row local solver (solver_dense.h)
     DevBuf gt, status;  // status: set by a Gram-solver launch whose hand-off timed out
+    DevBuf status_snap;  // status as of the rounds a pipelined evaluation covers (cocoa_eval_async)
     int32_t nbatch = 0;
     // Round t+1's samples and Gram rows are computed on gstream while round t's
     // solver runs (the sample sequence depends on seed + t only, the Gram rows
     // on the samples and the data): two (samples, gt) buffers, b and 1-b.
     DevBuf samples2, gt2;
+    // gram_seq_kernel's fallback windows: [0] count, then (partition, batch)
+    // pairs; one per Gram-row buffer (gt, gt2): round t+1's rows are formed on
+    // gstream while round t's may still be on the context's stream
+    DevBuf gram_fb[2];
+    int gram_chunks = 0;  // > 0: Gram rows by gram_seq_kernel, this many batch runs per partition
     hipStream_t gstream = nullptr;
     hipEvent_t g_ready = nullptr, s_done[2] = {nullptr, nullptr};
     int32_t pre_t = -1, pre_buf = 0;  // round prefetched into buffer pre_buf (-1: none)
@@ -1268,6 +1274,25 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         if (method != COCOA_METHOD_MBCD) {
             const size_t gtb = sizeof(double) * (size_t)K * (size_t)ctx->nbatch * 16 * 64;
             ctx->gt.alloc(gtb);
+            // Gram rows by runs of batches (gram_seq_kernel; COCOA_GRAM_SEQ=0: one
+            // workgroup per window, gram_kernel): its pool records hold the column
+            // in 27 bits and its links the batch in 18
+            {
+                const char* se = std::getenv("COCOA_GRAM_SEQ");
+                const bool seq = !(se && !std::atoi(se)) && ctx->d < ((int64_t)1 << 27) && ctx->nbatch < (1 << 18);
+                const char* ce = std::getenv("COCOA_GRAM_CHUNKS");
+                // runs per partition: one workgroup per CU on the CUs the solver's K
+                // workgroups leave (C2: 3; r06h A/B beside the solver: 1 run 5.1 ms,
+                // 2 runs 2.75, 3 runs 1.81, 4 runs 2.72 -- K * 4 = 256 workgroups
+                // need a second pass for the 64 that find no free CU)
+                const int kk = (int)std::max<int64_t>(K, 1);
+                const int autoc = std::max(1, std::min(8, (ncu - kk) / kk));
+                ctx->gram_chunks = !seq ? 0 : ce ? std::max(1, std::atoi(ce)) : autoc;
+                for (auto& fb : ctx->gram_fb) {
+                    if (seq) fb.alloc(sizeof(int32_t) * (1 + 2 * (size_t)K * (size_t)ctx->nbatch));
+                    else fb.free();
+                }
+            }
             // the next round's (samples, Gram rows) beside this round's, when they fit
             size_t free_b = 0, total_b = 0;
             HIPCHK(hipMemGetInfo(&free_b, &total_b));
@@ -1420,6 +1445,14 @@ static GramArgs gram_args(cocoa_ctx* c, const int32_t* samples, double* gt) {
     ga.nbatch = c->nbatch;
     ga.gt = gt;
     ga.prof = c->sa.prof ? c->sa.prof + (size_t)c->K_loc * kProfStride : nullptr;  // phase sums of this launch
+    ga.chunks = c->gram_chunks;
+    ga.fb_cap = (int32_t)((size_t)c->K_loc * (size_t)c->nbatch);
+    ga.nnz = c->tr.nnz;
+    ga.gt_len = (int64_t)c->K_loc * c->nbatch * 16 * 64;
+    ga.n_rows = c->tr.n;
+    DevBuf& fb = c->gram_fb[gt == c->gt2.as<double>() ? 1 : 0];
+    ga.fb_n = c->gram_chunks ? fb.as<int32_t>() : nullptr;
+    ga.fb = c->gram_chunks ? fb.as<int32_t>() + 1 : nullptr;
     return ga;
 }
 
@@ -1935,7 +1968,7 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
     bool host_done = false;  // the sums already stored to h_eval by the pass
     // the Gram solver's status word rides behind the pass (cocoa_eval_end /
     // cocoa_eval_wait raise on an aborted launch without a stream sync)
-    const bool gram_status = !ctx->strict && ctx->use_gram && ctx->status.p;
+    const bool gram_status = !ctx->strict && ctx->use_gram && ctx->status.p && (!async || ctx->status_snap.p);
     EvalArgs e{};
     e.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     e.col = ctx->tr.col.as<int32_t>();
@@ -1977,7 +2010,7 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
                 e.counter = cnt.as<unsigned>();
                 e.out_host = to_host ? ctx->h_eval + (async ? 4 : 0) : nullptr;
                 if (to_host && gram_status) {
-                    e.status = ctx->status.as<int>();
+                    e.status = async ? ctx->status_snap.as<int>() : ctx->status.as<int>();
                     e.status_host = (int*)(ctx->h_eval + (async ? 10 : 9));
                 }
                 host_done = launch_eval_fast(e, eval_fast_blocks(e.n_tiles, e.n_t_tiles), st);
@@ -1986,7 +2019,8 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
         }
     });
     if (to_host && gram_status && !host_done)
-        HIPCHK(hipMemcpyAsync(ctx->h_eval + (async ? 10 : 9), ctx->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(ctx->h_eval + (async ? 10 : 9), async ? ctx->status_snap.p : ctx->status.p, sizeof(int),
+                              hipMemcpyDeviceToHost, st));
     ctx->status_slot[async ? 1 : 0] = to_host && gram_status;
     if (async) {
         if (!host_done)
@@ -2110,6 +2144,10 @@ extern "C" int cocoa_eval_async(cocoa_ctx* ctx) {
     // raced the next round's plan and solver for CUs: 3.30 -> 3.74 ms per C2 step.)
     HIPCHK(hipMemcpyAsync(ctx->w_snap.p, ctx->w.p, nw, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(ctx->alpha_snap.p, ctx->alpha.p, na, hipMemcpyDeviceToDevice, ctx->stream));
+    if (ctx->use_gram && ctx->status.p) {  // the status word as of the evaluated rounds (the next round may set it)
+        if (!ctx->status_snap.p) ctx->status_snap.alloc(sizeof(int) * 4);
+        HIPCHK(hipMemcpyAsync(ctx->status_snap.p, ctx->status.p, sizeof(int), hipMemcpyDeviceToDevice, ctx->stream));
+    }
     HIPCHK(hipEventRecord(ctx->e_round, ctx->stream));
     ctx->eval_pending = true;
     ctx->eval_fired = false;
@@ -3133,6 +3171,36 @@ extern "C" int cocoa_solver_profile_read(cocoa_ctx* ctx, uint64_t* out, int64_t 
     CAPI_END(ctx)
 }
 
+extern "C" int cocoa_debug_gram_rows(cocoa_ctx* ctx, int32_t t, double* out, int64_t count) {
+    CAPI_BEGIN(ctx)
+    GROUP_REJECT(ctx, "cocoa_debug_gram_rows");
+    require(ctx->inited && ctx->use_gram && ctx->gt.p, COCOA_E_STATE,
+            "cocoa_debug_gram_rows: the context does not run the Gram-window solver with Gram rows");
+    const int32_t H = ctx->P.local_iters;
+    const int64_t need = (int64_t)ctx->K_loc * ctx->nbatch * 16 * 48;
+    require(out && count >= need, COCOA_E_ARG, "cocoa_debug_gram_rows: out holds fewer than K * nbatch * 16 * 48");
+    if (ctx->gstream) HIPCHK(hipStreamSynchronize(ctx->gstream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // a scratch sample / Gram buffer: the round state (and any prefetch) stays untouched
+    DevBuf smp, gt;
+    smp.alloc(sizeof(int32_t) * (size_t)ctx->samples_cap);
+    gt.alloc(sizeof(double) * (size_t)need);
+    launch_sampler(ctx->part_ptr.as<int64_t>(), ctx->K_loc, wrap32((int64_t)ctx->D.seed + t), H, smp.as<int32_t>(),
+                   ctx->jump.as<uint64_t>(), ctx->stream);
+    GramArgs ga = gram_args(ctx, smp.as<int32_t>(), gt.as<double>());
+    ga.prof = nullptr;
+    DevBuf fb;
+    if (ga.chunks > 0) {
+        fb.alloc(sizeof(int32_t) * (1 + 2 * (size_t)ctx->K_loc * (size_t)ctx->nbatch));
+        ga.fb_n = fb.as<int32_t>();
+        ga.fb = fb.as<int32_t>() + 1;
+    }
+    launch_gram(ga, ctx->stream);
+    HIPCHK(hipMemcpyAsync(out, gt.p, sizeof(double) * (size_t)need, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    CAPI_END(ctx)
+}
+
 extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
     CAPI_BEGIN(ctx)
     require(buf && len > 0, COCOA_E_ARG, "bad buffer");
@@ -3145,11 +3213,22 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
         std::memcpy(buf, p.c_str(), p.size() + 1);
         return COCOA_OK;
     }
+    // windows the last sequential Gram launch sent to the per-window kernel (diagnostic: waits for the side stream)
+    int32_t gfb = -1;
+    if (ctx->use_gram && ctx->gram_chunks > 0 && ctx->gram_fb[0].p) {
+        if (ctx->gstream) HIPCHK(hipStreamSynchronize(ctx->gstream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        int32_t f2[2] = {0, 0};
+        HIPCHK(hipMemcpy(&f2[0], ctx->gram_fb[0].p, sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (ctx->gram_fb[1].p) HIPCHK(hipMemcpy(&f2[1], ctx->gram_fb[1].p, sizeof(int32_t), hipMemcpyDeviceToHost));
+        gfb = std::max(f2[0], f2[1]);  // (the later of the two buffers' launches is not tracked: report the larger)
+    }
     std::snprintf(buf, (size_t)len,
-                  "{\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
+                  "{\"gram_chunks\":%d,\"gram_fallback_last\":%d,\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
                   "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d}",
+                  ctx->use_gram ? ctx->gram_chunks : 0, gfb,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,

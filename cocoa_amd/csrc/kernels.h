@@ -129,8 +129,17 @@ struct GramArgs {
     const double* val;
     int32_t K, H, nbatch;     // nbatch = ceil(H / 16)
     int32_t pad;
-    double* gt;               // [K][nbatch * 16][64]
+    double* gt;               // [K][nbatch * 16][48]
     uint64_t* prof;           // optional [8] phase cycles summed over the workgroups (diagnostics)
+    // sequential Gram rows (gram_seq_kernel): batch chunks per partition, and the
+    // fallback list of (partition, batch) windows its pool could not hold
+    // (fb: 2 int32 per window, capacity K * nbatch; fb_n: zeroed before the launch)
+    int32_t chunks;
+    int32_t fb_cap;           // pairs fb holds
+    int32_t* fb;
+    int32_t* fb_n;
+    int64_t nnz, gt_len;      // (bounds of col / val and gt: the checked debug variant)
+    int64_t n_rows;           // rows of row_ptr (+1 entries)
 };
 
 struct GramSolverArgs {
@@ -266,6 +275,7 @@ void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 // when it fits, else in alpha_work)
 size_t gram_solver_lds(int64_t d, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
+size_t gram_seq_lds();  // LDS bytes of gram_seq_kernel (one workgroup per CU)
 void launch_xw_produce(const XwArgs& a, hipStream_t s);
 void launch_xw_gather(const int64_t* part_ptr, const int32_t* samples, int32_t H, int64_t steps,
                       const double* row_xw, double* xw, hipStream_t s);

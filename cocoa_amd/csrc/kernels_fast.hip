@@ -30,16 +30,32 @@ size_t gram_solver_lds(int64_t d, int32_t* hot) {
     return base + sizeof(double) * (size_t)h;
 }
 
+// Gram rows of a round.  a.chunks > 0: gram_seq_kernel (K * chunks workgroups,
+// each a run of one partition's batches), then gram_list_kernel over the
+// windows its pool could not hold (usually none: the blocks read a zero count
+// and exit).  a.chunks == 0: gram_kernel, one workgroup per window.
 void launch_gram(const GramArgs& a, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)sizeof(GramLds));
+        (void)hipFuncSetAttribute((const void*)gram_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(GramLds));
+        (void)hipFuncSetAttribute((const void*)gram_seq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(GramSeqLds));
         attr = true;
     }
     const int64_t grid = (int64_t)a.K * a.nbatch;
-    if (grid > 0) gram_kernel<<<(unsigned)grid, kGramThreads, sizeof(GramLds), s>>>(a);
+    if (grid <= 0) return;
+    if (a.chunks > 0) {
+        (void)hipMemsetAsync(a.fb_n, 0, sizeof(int32_t), s);
+        gram_seq_kernel<<<(unsigned)((int64_t)a.K * a.chunks), kGsThreads, sizeof(GramSeqLds), s>>>(a);
+        gram_list_kernel<<<(unsigned)std::min<int64_t>(grid, 256), kGramThreads, sizeof(GramLds), s>>>(a);
+    } else {
+        gram_kernel<<<(unsigned)grid, kGramThreads, sizeof(GramLds), s>>>(a);
+    }
 }
+size_t gram_seq_lds() { return sizeof(GramSeqLds); }
 
 // x.w of the round's sampled rows beside the Gram solver, so that no evaluation
 // pass has to form them in line before the round (plan_impl.h forms the same

@@ -134,6 +134,14 @@ static __device__ double g_gram_one = 1.0;
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }    // vmcnt(0)
 __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F); }  // lgkmcnt(0)
 
+#ifdef COCOA_GS_CHECK  // debug variant: every global index checked (printf, access skipped)
+#define GS_OK(cond, what, v)                                                                              \
+    ((cond) ? true : (printf("gram_seq OOB %s %lld blk %d tid %d\n", what, (long long)(v), (int)blockIdx.x, \
+                             (int)threadIdx.x), false))
+#else
+#define GS_OK(cond, what, v) ((void)(v), true)
+#endif
+
 // ================================================================ Gram ==
 // Gt[k][j][slot] = x_s . x_j for the step s of window slot `slot` in j's
 // window [16 floor(j/16), +kGW) with s > j; 0 otherwise.
@@ -182,9 +190,8 @@ static_assert(kGramNU % 4 == 0, "gram_kernel probes four units at a time");
 __device__ __forceinline__ uint32_t gram_hash(int32_t c) { return ((uint32_t)c * 2654435761u) >> 20; }  // 12 bits
 static_assert(kGramTable <= 4096 && kGramTile <= 32767, "gram_hash bits / int16 list links");
 
-__global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-    GramLds& L = *(GramLds*)lds_raw;
+// Gram rows of one updater batch g of partition k (every thread of the block)
+__device__ __forceinline__ void gram_batch(const GramArgs& a, GramLds& L, int k, int g) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     uint64_t tph = a.prof ? __builtin_readcyclecounter() : 0;
     auto phase = [&](int i) {  // diagnostics: thread 0 adds the phase's cycles
@@ -194,21 +201,6 @@ __global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a
             tph = t;
         }
     };
-    // XCD-aware order: blocks land on the 8 XCDs round robin; one partition's
-    // consecutive batches (3/4 of their partners shared) stay on one XCD, close
-    // in time, so its L2 serves the re-reads
-    int k, g;
-    {
-        const int64_t b = blockIdx.x;
-        if (a.K % 8 == 0) {
-            const int64_t kx = a.K / 8, i = b / 8;
-            k = (int)((b % 8) + 8 * (i % kx));
-            g = (int)(i / kx);
-        } else {
-            k = (int)(b % a.K);
-            g = (int)(b / a.K);
-        }
-    }
     const int32_t H = a.H;
     const int32_t j0 = g * kGB;
     const int32_t P = min(kGW, H - j0);         // partners [j0, j0 + P)
@@ -423,6 +415,376 @@ __global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a
         if (lane < kGW) __builtin_nontemporal_store(v, out + (size_t)u * kGW + slot);
     }
     phase(4);
+}
+
+__global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_kernel(GramArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    GramLds& L = *(GramLds*)lds_raw;
+    // XCD-aware order: blocks land on the 8 XCDs round robin; one partition's
+    // consecutive batches (3/4 of their partners shared) stay on one XCD, close
+    // in time, so its L2 serves the re-reads
+    int k, g;
+    {
+        const int64_t b = blockIdx.x;
+        if (a.K % 8 == 0) {
+            const int64_t kx = a.K / 8, i = b / 8;
+            k = (int)((b % 8) + 8 * (i % kx));
+            g = (int)(i / kx);
+        } else {
+            k = (int)(b % a.K);
+            g = (int)(b / a.K);
+        }
+    }
+    gram_batch(a, L, k, g);
+}
+
+// The same rows for a list of (partition, batch) pairs: the windows the
+// sequential kernel below could not hold in its LDS pool (fb_n of them, at
+// fb[2 i], fb[2 i + 1]); a block per pair, grid-stride.
+__global__ __launch_bounds__(kGramThreads, kGramWGs) void gram_list_kernel(GramArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    GramLds& L = *(GramLds*)lds_raw;
+    const int32_t n = *a.fb_n;
+    for (int32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        if (!GS_OK(i < a.fb_cap && a.fb[2 * i] >= 0 && a.fb[2 * i] < a.K && a.fb[2 * i + 1] >= 0 &&
+                       a.fb[2 * i + 1] < a.nbatch, "fb pair", i))
+            continue;
+        gram_batch(a, L, a.fb[2 * i], a.fb[2 * i + 1]);
+        __syncthreads();  // (LDS reused by the next pair)
+    }
+}
+
+// ===================================================== Gram rows, sequential ==
+// gram_seq_kernel: one workgroup walks a contiguous chunk of one partition's
+// batches in order and keeps the window's rows in LDS, so each batch is loaded,
+// hashed and imaged once instead of once per window that holds it (three
+// times), and each cold updater entry makes ONE lookup for the whole window
+// instead of every partner entry probing the updaters' hash:
+//
+//   pool   -- the cold entries (device column >= kGHot) of the live batches
+//             x-2 .. x, a ring of kGsPool records {column | step-in-batch << 27,
+//             link, value}; batch x's entries at [pstart_x, pstart_x + n_x);
+//   head   -- one list per hash bucket, newest first.  A link holds the
+//             target's BATCH in its high bits (batch << 13 | slot), so a walk
+//             for updater batch g stops at the first link into a batch < g
+//             without reading it: entries of dead batches are never touched,
+//             and their ring slots are reused without unlinking anything;
+//   XP     -- the dense image of the hot columns, a ring of 4 batches x 16 rows;
+//             the hot products of updater batch g against partner batches g,
+//             g+1, g+2 are three 16 x 16 tiles over 48 columns on
+//             v_mfma_f64_16x16x4f64 (12 per tile), stored to accH;
+//   accC   -- the cold products, fp64 LDS atomics by the walks.
+//
+// Per batch x of the chunk (updater g = x - 2):
+//   B1  hot entries of x into XP; cold counts per (register unit, wave);
+//   B3  cold entries of x into the pool (ranks by a scan of the counts) and
+//       their lists; the next batch's entries issued into registers;
+//   C   MFMA tiles of g (waves 0-2); every wave walks g's cold entries;
+//   D   Gt rows of g (accH + accC, as gram_kernel writes them); XP rows of
+//       batch x+2 cleared; the batch metadata (row starts, packed offsets) of
+//       x+2 written, x+3 / x+4 loaded, by wave 0.
+// A batch whose cold entries do not fit the pool beside the two before it is
+// not inserted; the windows that hold it (updaters x-2, x-1, x) go to the
+// fallback list, recomputed afterwards by gram_list_kernel (the per-window
+// kernel, any size).
+// (r06i A/B, C2 beside the solver, 3 runs per partition: 512 threads and 48 hot
+// columns 1.80 ms; 1,024 threads 1.24; 96 hot columns 1.57; both 1.16)
+#ifndef COCOA_GS_THREADS
+#define COCOA_GS_THREADS 1024
+#endif
+#ifndef COCOA_GS_HOT
+#define COCOA_GS_HOT 96
+#endif
+constexpr int kGsThreads = COCOA_GS_THREADS;
+constexpr int kGsWaves = kGsThreads / 64;
+constexpr int kGsNU = 3072 / kGsThreads; // register units of kGsThreads entries: 3,072 entries of a batch at once
+constexpr int kGsHot = COCOA_GS_HOT;     // dense (MFMA) columns: device order, most frequent first
+constexpr int kGsHotS = kGsHot + 1;
+#ifndef COCOA_GS_POOL
+#define COCOA_GS_POOL 4608
+#endif
+// cold-entry ring: C2 windows hold 2,300 cold entries (column >= 96) on average,
+// ~3,700 for 99.9% of them, so a handful per round go to the fallback list
+constexpr int kGsPool = COCOA_GS_POOL;
+constexpr int kGsSlotBits = 13;
+static_assert(kGsPool <= (1 << kGsSlotBits), "link slot bits");
+constexpr int kGsBuckets = 4096;         // gram_hash: 12 bits
+constexpr int kGsMeta = 8;               // batch metadata ring
+constexpr int kGsAhead = 3;              // batches whose entries are in flight (register sets)
+static_assert(kGsAhead + 4 <= kGsMeta, "live metadata: batches x-2 .. x+kGsAhead+1");
+constexpr int kGsColBits = 27;           // column bits of a pool record (step-in-batch above)
+struct GsMetaRec {
+    int64_t beg[kGB];                    // row starts of the batch's 16 steps
+    int32_t pref[kGB + 1];               // packed offsets (entries of steps < i)
+    int32_t pstart, pn;                  // the batch's cold entries in the pool
+};
+struct GramSeqLds {
+    // pool records, split so a walk reads 8 bytes per visited record and the
+    // value only on a column match: pcn = {column | step-in-batch << 27, link}
+    int2 pcn[kGsPool];
+    double pval[kGsPool];
+    int32_t head[kGsBuckets];
+    double XP[4 * kGB][kGsHotS];         // hot image, row = 16 (batch % 4) + step-in-batch
+    double accH[kGB][kGW];
+    double accC[kGB][kGW];
+    GsMetaRec meta[kGsMeta];
+    int32_t cnt[kGsNU * kGsWaves];
+};
+static_assert(sizeof(GramSeqLds) <= 160 * 1024, "gram_seq_kernel LDS");
+static_assert(kGsNU * kGsWaves <= 64, "one lane per (unit, wave) count");
+static_assert(kGsHot % 4 == 0, "MFMA k-steps of 4 hot columns");
+static_assert(kGW == 3 * kGB, "three partner batches (MFMA tiles)");
+
+typedef double gs_d4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(kGsThreads, 1) void gram_seq_kernel(GramArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    GramSeqLds& L = *(GramSeqLds*)lds_raw;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // block b: partition b % K (the solver's XCD when K % 8 == 0), chunk b / K
+    const int k = (int)(blockIdx.x % (unsigned)a.K), ch = (int)(blockIdx.x / (unsigned)a.K);
+    const int32_t H = a.H, NB = a.nbatch;
+    const int32_t gA = (int32_t)(((int64_t)NB * ch) / a.chunks), gB = (int32_t)(((int64_t)NB * (ch + 1)) / a.chunks);
+    if (gA >= gB) return;
+    const int64_t p0 = a.part_ptr[k];
+    const int32_t* smp = a.samples + (size_t)k * H;
+    double* gtk = a.gt + (size_t)k * NB * kGB * kGW;
+
+    for (int i = tid; i < kGsBuckets; i += kGsThreads) L.head[i] = -1;
+    for (int i = tid; i < 4 * kGB * kGsHotS; i += kGsThreads) (&L.XP[0][0])[i] = 0.0;
+    for (int i = tid; i < kGB * kGW; i += kGsThreads) (&L.accC[0][0])[i] = 0.0;
+
+    // ---- batch metadata (wave 0, lanes 0..15 = steps): samples -> row extents ----
+    // in flight: row extents of batch mx (rb, re), samples of batch mx + 1 (ms)
+    struct Ext {
+        int64_t b, e;
+    };
+    Ext rx{0, 0};
+    int32_t ms = -1;
+    auto smp_of = [&](int32_t x) -> int32_t {  // sample of step lane of batch x (-1: none)
+        const int32_t j = x * kGB + lane;
+        return (lane < kGB && x < NB && j < H && GS_OK(j >= 0, "smp", j)) ? smp[j] : -1;
+    };
+    auto extents = [&](int32_t r) -> Ext {
+        const bool ok = r >= 0 && GS_OK(p0 + r + 1 <= a.n_rows, "row_ptr", p0 + r);
+        const int64_t i = ok ? p0 + r : 0;
+        const int64_t b = a.row_ptr[i], e = a.row_ptr[i + 1];
+        return ok ? Ext{b, e} : Ext{0, 0};
+    };
+    auto meta_write = [&](int32_t x, const Ext& q) {  // batch x's metadata from its row extents
+        GsMetaRec& M = L.meta[x & (kGsMeta - 1)];
+        const int32_t z = lane < kGB ? (int32_t)(q.e - q.b) : 0;
+        const int32_t inc = wave_incl_scan(z);
+        if (lane < kGB) {
+            M.beg[lane] = q.b;
+            M.pref[lane + 1] = inc;
+        }
+        if (lane == 0) M.pref[0] = 0;
+    };
+    // metadata kGsAhead + 1 batches ahead, entries kGsAhead batches ahead (registers)
+    if (wv == 0) {
+#pragma unroll
+        for (int32_t i = 0; i <= kGsAhead; ++i) meta_write(gA + i, extents(smp_of(gA + i)));
+        rx = extents(smp_of(gA + kGsAhead + 1));  // written in the first D phase
+        ms = smp_of(gA + kGsAhead + 2);
+        if (lane == 0) {
+            L.meta[(gA - 1) & (kGsMeta - 1)].pstart = 0;  // the pool starts empty
+            L.meta[(gA - 1) & (kGsMeta - 1)].pn = 0;
+            L.meta[(gA - 2) & (kGsMeta - 1)].pn = 0;
+        }
+    }
+    __syncthreads();
+
+    // ---- a batch's entries in registers: q = u * kGsThreads + tid ----
+    struct Ents {
+        int32_t col[kGsNU];
+        double val[kGsNU];
+        int8_t own[kGsNU];
+    };
+    auto issue = [&](Ents& E, int32_t x) {  // entries [0, kGsNU * kGsThreads) of batch x
+        const GsMetaRec& M = L.meta[x & (kGsMeta - 1)];
+        const int32_t T = x < NB ? M.pref[kGB] : 0;
+#pragma unroll
+        for (int u = 0; u < kGsNU; ++u) {
+            const int32_t q = u * kGsThreads + tid;
+            int lo = 0;
+            if (q < T) {
+#pragma unroll
+                for (int st = kGB / 2; st >= 1; st >>= 1)
+                    if (M.pref[lo + st] <= q) lo += st;
+            }
+            E.own[u] = (int8_t)(q < T ? lo : -1);
+        }
+#pragma unroll
+        for (int u = 0; u < kGsNU; ++u) {
+            const int o = E.own[u];
+            const int32_t q = u * kGsThreads + tid;
+            const int64_t e = o >= 0 ? M.beg[o] + (q - M.pref[o]) : 0;
+            const bool ok = o >= 0 && GS_OK(e >= 0 && e < a.nnz, "entry", e);
+            E.col[u] = ok ? a.col[e] : -1;
+            E.val[u] = ok ? a.val[e] : 0.0;
+        }
+    };
+    static_assert(kGsAhead == 3, "the main loop rotates three register sets");
+    Ents E0, E1, E2;
+    issue(E0, gA);
+    issue(E1, gA + 1);
+    issue(E2, gA + 2);
+
+    const uint64_t below = (1ull << lane) - 1;
+    int32_t fb_next = gA;  // (thread 0) windows before it are on the fallback list already
+    // diagnostics (a.prof): thread 0's cycles per phase, summed in registers and
+    // added to the launch's totals once at the end (one atomic per phase and block)
+    uint64_t tph = a.prof ? __builtin_readcyclecounter() : 0;
+    uint64_t pc[7] = {0, 0, 0, 0, 0, 0, 0};
+    auto phase = [&](int i) {
+        if (a.prof && tid == 0) {
+            const uint64_t t = __builtin_readcyclecounter();
+            pc[i] += t - tph;
+            tph = t;
+        }
+    };
+    // one batch x (insert x, Gram rows of updater batch g = x - 2); E holds batch
+    // x's entries and is refilled with batch x + kGsAhead's
+    auto step = [&](const int32_t x, Ents& E) {
+        const int32_t g = x - 2;
+        const bool ins = x < NB;
+        const int32_t T = ins ? L.meta[x & (kGsMeta - 1)].pref[kGB] : 0;
+        const int xs = x & 3;
+        // batch x's cold entries go in after the live ones of x-2, x-1
+        const GsMetaRec& Mp = L.meta[(x - 1) & (kGsMeta - 1)];
+        const int32_t base = (Mp.pstart + Mp.pn) % kGsPool;
+        const int32_t live = Mp.pn + L.meta[(x - 2) & (kGsMeta - 1)].pn;
+        // a batch longer than one register chunk is never inserted (fallback windows)
+        bool ovf = T > kGsNU * kGsThreads;
+        int32_t tot = 0;
+        const bool body = T > 0 && !ovf;
+        // B1: hot entries into the image; cold counts per (unit, wave)
+        uint64_t m[kGsNU];
+#pragma unroll
+        for (int u = 0; u < kGsNU; ++u) {
+            const int32_t c = body ? E.col[u] : -1;
+            if (c >= 0 && c < kGsHot) atomicAdd(&L.XP[xs * kGB + E.own[u]][c], E.val[u]);
+            m[u] = __ballot(c >= kGsHot);
+            if (lane == 0) L.cnt[u * kGsWaves + wv] = __popcll(m[u]);
+        }
+        phase(0);
+        // (every iteration: it also orders wave 0's metadata written in the last D
+        // phase before the reads of issue() below)
+        __syncthreads();
+        phase(1);
+        if (body) {
+            // B3: ranks (every wave scans the counts itself) and the pool records
+            const int32_t cv = lane < kGsNU * kGsWaves ? L.cnt[lane] : 0;
+            const int32_t inc = wave_incl_scan(cv);
+            tot = __shfl(inc, 63, 64);
+            ovf = live + tot > kGsPool;
+            if (!ovf) {
+#pragma unroll
+                for (int u = 0; u < kGsNU; ++u) {
+                    const int32_t ex = __shfl(inc - cv, u * kGsWaves + wv, 64);
+                    if ((m[u] >> lane) & 1) {
+                        const int32_t slot = (base + ex + __popcll(m[u] & below)) % kGsPool;
+                        const int32_t c = E.col[u];
+                        const int32_t link = (x << kGsSlotBits) | slot;
+                        const int32_t old = atomicExch(&L.head[gram_hash(c) & (kGsBuckets - 1)], link);
+                        L.pcn[slot] = make_int2(c | ((int32_t)E.own[u] << kGsColBits), old);
+                        L.pval[slot] = E.val[u];
+                    }
+                }
+            }
+        }
+        if (wv == 0 && lane == 0 && ins) {
+            GsMetaRec& M = L.meta[x & (kGsMeta - 1)];
+            M.pstart = base;
+            M.pn = ovf ? 0 : tot;
+            if (ovf) {  // windows holding batch x: recomputed by gram_list_kernel (each once)
+                for (int32_t y = max(max(x - 2, gA), fb_next); y <= min(x, gB - 1); ++y) {
+                    fb_next = y + 1;
+                    const int32_t i = atomicAdd(a.fb_n, 1);
+                    if (GS_OK(i < a.fb_cap, "fb", i)) {
+                        a.fb[2 * i] = k;
+                        a.fb[2 * i + 1] = y;
+                    }
+                }
+            }
+        }
+        // batch x + kGsAhead's entries, in flight through the next kGsAhead batches
+        issue(E, x + kGsAhead);
+        phase(2);
+        __syncthreads();  // (pool, lists, meta of x)
+        phase(3);
+        if (g >= gA) {
+            // C: hot tiles on MFMA (waves 0..2: partner batch g + wv), then the cold walk
+            const int gs = g & 3;
+            if (wv < 3) {
+                const int ps = (g + wv) & 3;
+                gs_d4 acc = {0.0, 0.0, 0.0, 0.0};
+                const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+                for (int kk = 0; kk < kGsHot / 4; ++kk) {
+                    const double av = L.XP[gs * kGB + r][4 * kk + kq];
+                    const double bv = L.XP[ps * kGB + r][4 * kk + kq];
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) L.accH[kq + 4 * i][wv * kGB + r] = acc[i];
+            }
+            const GsMetaRec& Mg = L.meta[g & (kGsMeta - 1)];
+            const int32_t n = Mg.pn, ps0 = Mg.pstart;
+            for (int32_t i = tid; i < n; i += kGsThreads) {
+                const int32_t se = (ps0 + i) % kGsPool;
+                const int32_t ecu = L.pcn[se].x;
+                const double ev = L.pval[se];
+                const int32_t c = ecu & ((1 << kGsColBits) - 1), u = ecu >> kGsColBits;
+                int32_t l = L.head[gram_hash(c) & (kGsBuckets - 1)];
+                while (l >= 0 && (l >> kGsSlotBits) >= g) {
+                    const int32_t sf = l & ((1 << kGsSlotBits) - 1);
+                    const int2 f = L.pcn[sf];
+                    if ((f.x & ((1 << kGsColBits) - 1)) == c) {
+                        const int32_t p = ((l >> kGsSlotBits) - g) * kGB + (f.x >> kGsColBits);
+                        if (p > u) atomicAdd(&L.accC[u][p], ev * L.pval[sf]);
+                    }
+                    l = f.y;
+                }
+            }
+        }
+        phase(4);
+        __syncthreads();  // (accH, accC)
+        phase(5);
+        // D: Gt rows of g; XP rows of batch x+2 cleared (they held x-2 = g); metadata
+        if (g >= gA) {
+            const int32_t j0 = g * kGB, U = min(kGB, H - j0), P = min(kGW, H - j0);
+            double* out = gtk + (size_t)j0 * kGW;
+            for (int i = tid; i < kGB * kGW; i += kGsThreads) {
+                const int u = i / kGW, p = i - u * kGW;
+                const double v = (u < U && p > u && p < P) ? L.accH[u][p] + L.accC[u][p] : 0.0;
+                const int64_t oi = (int64_t)(out - a.gt) + (int64_t)u * kGW + (j0 + p) % kGW;
+                if (GS_OK(oi >= 0 && oi < a.gt_len, "gt", oi))
+                    __builtin_nontemporal_store(v, out + (size_t)u * kGW + (j0 + p) % kGW);
+                L.accC[u][p] = 0.0;
+            }
+        }
+        {
+            const int cs = (x + 2) & 3;
+            for (int i = tid; i < kGB * kGsHotS; i += kGsThreads) (&L.XP[cs * kGB][0])[i] = 0.0;
+        }
+        if (wv == 0) {
+            meta_write(x + kGsAhead + 1, rx);  // row extents loaded one batch ago
+            rx = extents(ms);                  // batch x + kGsAhead + 2
+            ms = smp_of(x + kGsAhead + 3);
+        }
+        phase(6);
+        // (no barrier: the next B1 writes XP rows of x+1, cleared one batch ago, and
+        // reads nothing D writes; its first barrier orders the rest)
+    };
+    for (int32_t x = gA; x < gB + 2; x += 3) {
+        step(x, E0);
+        if (x + 1 < gB + 2) step(x + 1, E1);
+        if (x + 2 < gB + 2) step(x + 2, E2);
+    }
+    if (a.prof && tid == 0)
+        for (int i = 0; i < 7; ++i) atomicAdd((unsigned long long*)&a.prof[i], (unsigned long long)pc[i]);
 }
 
 // ============================================================== solver ==

@@ -321,6 +321,15 @@ class Engine:
                                                   len(out)), self.h)
         return out.reshape(self.K_loc, 2, 16) if count is None else out
 
+    def gram_rows(self, t):
+        """cocoa_debug_gram_rows: round t's Gram rows, shape [K_loc, nbatch * 16, 48]."""
+        p = self.plan()
+        K, H = p["K_loc"], self.params.local_iters
+        nb = (H + 15) // 16
+        out = np.zeros(K * nb * 16 * 48, np.float64)
+        C.check(C.lib().cocoa_debug_gram_rows(self.h, int(t), C.f64p(out), out.size), self.h)
+        return out.reshape(K, nb * 16, 48)
+
     def plan(self):
         buf = ctypes.create_string_buffer(1024)
         C.check(C.lib().cocoa_plan_info(self.h, buf, 1024), self.h)

@@ -325,6 +325,12 @@ int cocoa_solver_profile(cocoa_ctx *ctx, int enable);
 int cocoa_solver_profile_read(cocoa_ctx *ctx, uint64_t *out, int64_t count);
 /* Human-readable description of how the solver was planned (LDS placement). */
 int cocoa_plan_info(cocoa_ctx *ctx, char *buf, int len);
+/* Diagnostics (fast mode, Gram-window solver, not MbCD): the Gram rows of round
+ * t's sampled steps (seed = DebugParams.seed + t) as the next cocoa_round(t)
+ * would use them, into out[count]: [K_loc][ceil(H/16) * 16][48] doubles, row j
+ * holding x_s . x_j at slot s % 48 for the steps s after j in its 48-step
+ * window, 0 elsewhere.  Synchronises the context. */
+int cocoa_debug_gram_rows(cocoa_ctx *ctx, int32_t t, double *out, int64_t count);
 int cocoa_sync(cocoa_ctx *ctx);
 
 /* ---- host-side data layer (no device needed) ---------------------------- */

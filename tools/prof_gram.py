@@ -30,8 +30,10 @@ def main():
     allp = e.solver_profile_read(e.K_loc * S + 8).astype(np.float64)
     full = allp[:e.K_loc * S].reshape(e.K_loc, S)
     nwg = e.K_loc * ((sh.H + 15) // 16)
-    gram_phases = dict(zip(["meta_zero", "load_hot_image", "-", "hot_product", "store", "cold_insert", "cold_probe", "-"],
-                           (allp[e.K_loc * S:e.K_loc * S + 8] / nwg).tolist()))
+    seq = e.plan().get("gram_chunks", 0) > 0
+    names = (["B1_hot_counts(+E wait)", "bar1", "B3_insert+issue", "bar2", "C_mfma_walk", "bar3", "D_store_meta", "-"]
+             if seq else ["meta_zero", "load_hot_image", "-", "hot_product", "store", "cold_insert", "cold_probe", "-"])
+    gram_phases = dict(zip(names, (allp[e.K_loc * S:e.K_loc * S + 8] / nwg).tolist()))  # per batch (seq: per batch and run)
     # solver_gram.h: [k][64] = wave w at 4 w (wait cycles, total cycles), memory
     # wave c's phase cycles at 48 + 4 c; roles in the default layout (COCOA_GLAYOUT)
     raw = full[:, :24].reshape(e.K_loc, 6, 4)

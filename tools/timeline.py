@@ -12,7 +12,7 @@ import sys
 
 
 def short(name):
-    for key, tag in (("solver_gram", "solver"), ("gram_kernel", "gram"), ("xw_produce", "xw"),
+    for key, tag in (("solver_gram", "solver"), ("gram_seq", "gram_seq"), ("gram_list", "gram_list"), ("gram_kernel", "gram"), ("xw_produce", "xw"),
                      ("eval_stream", "eval"), ("eval_final", "eval_fin"), ("plan_kernel", "plan"),
                      ("fold", "fold"), ("sampler", "sampler"), ("copyBuffer", "copy"), ("fillBuffer", "fill")):
         if key in name:
