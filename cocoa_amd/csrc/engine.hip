@@ -255,6 +255,9 @@ struct cocoa_ctx {
     // gstream while round t's may still be on the context's stream
     DevBuf gram_fb[2];
     int gram_chunks = 0;  // > 0: Gram rows by gram_seq_kernel, this many batch runs per partition
+    bool gram_mirror = false;  // the Gram solver as two workgroups per partition (solver_gram.h MIRROR)
+    DevBuf xbase;              //   their partial-base exchange ([K][4][kXbR][16][2] tagged granules)
+    int32_t xtag_epoch = 0;    //   launch counter in the granule tags
     hipStream_t gstream = nullptr;
     hipEvent_t g_ready = nullptr, s_done[2] = {nullptr, nullptr};
     int32_t pre_t = -1, pre_buf = 0;  // round prefetched into buffer pre_buf (-1: none)
@@ -876,8 +879,8 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
         pcol.resize((size_t)std::max<int64_t>(nnz, 1));
         for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];
     }
-    // Fast mode: every row stores its entries class by class (class of device
-    // column c = c % kGramClasses), each class in stored order, so that each of
+    // Fast mode: every row stores its entries in four runs (device column
+    // c % kGramRuns), each in stored order, so that each of
     // the Gram solver's memory waves (solver_gram.h) streams one contiguous run
     // per row.  Only the fast kernels see this order (their dots are
     // reassociated anyway); strict mode keeps the stored order of every row.
@@ -888,7 +891,7 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     // LDS-resident columns vs the rest, or the columns holding the first half of
     // the entries vs the rest -- measured 3.93 / 2.97 ms against 2.70: the first
     // class's fetch and memory waves carry most of the units; r03 A/B)
-    auto class_of = [&](int32_t c) -> int { return c % kGramClasses; };
+    auto class_of = [&](int32_t c) -> int { return c % kGramRuns; };
     if (split_classes) {
         pval.resize((size_t)nnz);
         zcv.resize((size_t)std::max<int64_t>(n_rows, 1) * 4);
@@ -899,15 +902,15 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
             th.emplace_back([&, tix] {
                 for (int64_t r = n_rows * tix / T; r < n_rows * (tix + 1) / T; ++r) {
                     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
-                    int64_t cnt[kGramClasses] = {}, at[kGramClasses];
+                    int64_t cnt[kGramRuns] = {}, at[kGramRuns];
                     for (int64_t q = b; q < e; ++q) ++cnt[class_of(pcol[(size_t)q])];
                     int64_t run = b;
-                    for (int c = 0; c < kGramClasses; ++c) {
+                    for (int c = 0; c < kGramRuns; ++c) {
                         at[c] = run;
                         run += cnt[c];
                     }
-                    for (int c = 0; c < 4; ++c)  // ends of the class runs (row-relative); unused: z
-                        zcv[(size_t)r * 4 + c] = (int32_t)((c < kGramClasses - 1 ? at[c] + cnt[c] : e) - b);
+                    for (int c = 0; c < 4; ++c)  // ends of runs 0..2 (row-relative), then the row length
+                        zcv[(size_t)r * 4 + c] = (int32_t)((c < kGramRuns - 1 ? at[c] + cnt[c] : e) - b);
                     for (int64_t q = b; q < e; ++q) {
                         const int64_t dst = at[class_of(pcol[(size_t)q])]++;
                         ncol[(size_t)dst] = pcol[(size_t)q];
@@ -1153,7 +1156,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         HIPCHK(hipMemsetAsync(ctx->w.p, 0, sizeof(double) * (size_t)d, s));
     ctx->alpha.alloc_zero(sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
     ctx->alpha_oob = false;
-    ctx->alpha_work.alloc(sizeof(double) * (size_t)(std::max<int64_t>(n, 1) + K));  // + a sink per partition
+    // + a sink per partition; two copies (the mirrored Gram solver's halves each keep their own)
+    ctx->alpha_work.alloc(2 * sizeof(double) * (size_t)(std::max<int64_t>(n, 1) + K));
     if (ctx->zstream) HIPCHK(hipStreamSynchronize(ctx->zstream));  // no re-zeroing in flight
     ctx->gram_quiesce();                                            // no Gram prefetch in flight
     ctx->eval_quiesce();                                            // nor a pending evaluation
@@ -1268,6 +1272,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                     (ctx->solver_kind == COCOA_SOLVER_GRAM ||
                      (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0 && K <= ncu));
     ctx->use_plan = is_sdca(method) || ctx->use_gram;
+    ctx->gram_mirror = false;
     if (ctx->use_gram) {
         ctx->status.alloc_zero(sizeof(int) * 4, s);
         ctx->nbatch = (H + 15) / 16;  // kGB = 16 steps per batch (solver_gram.h)
@@ -1286,7 +1291,16 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                 // 2 runs 2.75, 3 runs 1.81, 4 runs 2.72 -- K * 4 = 256 workgroups
                 // need a second pass for the 64 that find no free CU)
                 const int kk = (int)std::max<int64_t>(K, 1);
-                const int autoc = std::max(1, std::min(8, (ncu - kk) / kk));
+                // the mirrored solver (CoCoA+ / CoCoA, 4 K <= CUs; COCOA_GRAM_MIRROR=0 turns it
+                // off): two workgroups per partition, the Gram rows on the rest.  C2 (r06l,
+                // one box): solver 2.62 -> 2.39 ms, step 2.92 -> 2.70
+                const char* me = std::getenv("COCOA_GRAM_MIRROR");
+                ctx->gram_mirror = !(me && !std::atoi(me)) && 4 * kk <= ncu && !ctx->dw_compact && ctx->row_zc.p &&
+                                   (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_COCOA);
+                if (ctx->gram_mirror) ctx->xbase.alloc_zero(sizeof(uint64_t) * (size_t)kk * kGramRuns * kXbR * 32, s);
+                else ctx->xbase.free();
+                const int used = (ctx->gram_mirror ? 2 : 1) * kk;
+                const int autoc = std::max(1, std::min(8, (ncu - used) / kk));
                 ctx->gram_chunks = !seq ? 0 : ce ? std::max(1, std::atoi(ce)) : autoc;
                 for (auto& fb : ctx->gram_fb) {
                     if (seq) fb.alloc(sizeof(int32_t) * (1 + 2 * (size_t)K * (size_t)ctx->nbatch));
@@ -1641,6 +1655,11 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.w = c->w.as<double>();
             g.lambda = c->P.lambda;
             g.t0 = lsgd_t0;
+            g.alpha_work_stride = c->tr.n + K;
+            g.mirror = c->gram_mirror ? 1 : 0;
+            g.xbase = c->xbase.as<uint64_t>();
+            if (c->gram_mirror) c->xtag_epoch = (c->xtag_epoch % 4095) + 1;  // 1..4095 (12 tag bits, never 0)
+            g.xtag_epoch = c->xtag_epoch;
             const int mode = c->method == COCOA_METHOD_LOCALSGD ? MODE_LSGD : solver_mode(c->method);
             c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(mode, g, K, s); });
             // fault injection for the abort-reporting tests: COCOA_INJECT_ABORT=t
@@ -3224,11 +3243,11 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
         gfb = std::max(f2[0], f2[1]);  // (the later of the two buffers' launches is not tracked: report the larger)
     }
     std::snprintf(buf, (size_t)len,
-                  "{\"gram_chunks\":%d,\"gram_fallback_last\":%d,\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
+                  "{\"gram_chunks\":%d,\"gram_fallback_last\":%d,\"gram_mirror\":%d,\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
                   "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d}",
-                  ctx->use_gram ? ctx->gram_chunks : 0, gfb,
+                  ctx->use_gram ? ctx->gram_chunks : 0, gfb, ctx->gram_mirror ? 1 : 0,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,

@@ -14,15 +14,20 @@ namespace cocoa {
 enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2, MODE_LSGD = 3 };
 
 constexpr int kWave = 64;
-// deltaW column classes of the Gram solver (solver_gram.h): device column c is
-// in class c % kGramClasses, each with its own memory and fetch wave.  In fast
-// mode every row stores its entries class by class (cocoa_set_train), with the
-// run ends of classes 0 .. kGramClasses-2 per row in row_zc (4 int32 a row).
+// deltaW column classes of the Gram solver (solver_gram.h).  In fast mode every
+// row stores its entries in four runs by device column c % kGramRuns
+// (cocoa_set_train), with the ends of runs 0 .. 2 per row in row_zc (4 int32 a
+// row: three ends and the row length).  A solver workgroup has kGramClasses
+// memory / fetch waves: class lc of the one-workgroup solver takes runs 2 lc and
+// 2 lc + 1 (c % 4 in {2 lc, 2 lc + 1}); the mirrored solver's half h (two
+// workgroups per partition) takes run 2 lc + h, so half h owns the columns of
+// parity h.
 #ifndef COCOA_GNC
 #define COCOA_GNC 2
 #endif
 constexpr int kGramClasses = COCOA_GNC;
-static_assert(kGramClasses == 2 || kGramClasses == 4, "column classes");
+static_assert(kGramClasses == 2, "column classes per workgroup");
+constexpr int kGramRuns = 4;        // column runs of a fast-mode row (c % 4)
 constexpr int kProfStride = 64;     // solver profile words per partition (diagnostics)
 constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
 #ifndef COCOA_REG_CHUNKS
@@ -180,7 +185,16 @@ struct GramSolverArgs {
     int32_t xw_epoch;
     int32_t xw_pad;
     int64_t xw_stride;
+    // mirrored solver (two workgroups per partition, grid 2 K; half h = blockIdx /
+    // K owns the deltaW columns of parity h): each half's partial bases of a
+    // batch go to the other through xbase (tagged 8-byte granules, tag =
+    // xtag_epoch << 20 | batch + 1), its working alpha at alpha_work + h (n + K)
+    int32_t mirror;
+    int32_t xtag_epoch;
+    uint64_t* xbase;          // [K][kGramRuns][kXbR][kGB][2]
+    int64_t alpha_work_stride;  // n + K (mirror)
 };
+constexpr int kXbR = 8;     // xbase ring (batches)
 
 // x.w of the round's sampled rows, produced beside the Gram solver (its loader
 // polls the flags): one 256-thread block per (batch, partition), batch-major

@@ -96,6 +96,15 @@ void launch_xw_produce(const XwArgs& a, hipStream_t s) {
 
 template <int MODE, bool HOTLDS, bool PROJ, int XWM>
 static void launch_sg4(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
+    // the mirrored form (two workgroups per partition): CoCoA+ / CoCoA, hot
+    // columns in LDS; the caller sets a.mirror only then
+    constexpr bool MIR_OK = (MODE == MODE_PLUS || MODE == MODE_COCOA) && HOTLDS;
+    if (MIR_OK && a.mirror) {
+        (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XWM, MIR_OK>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        solver_gram_kernel<MODE, HOTLDS, PROJ, XWM, MIR_OK><<<2 * grid, kGThreads + 64, lds, s>>>(a);
+        return;
+    }
     (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XWM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     solver_gram_kernel<MODE, HOTLDS, PROJ, XWM><<<grid, kGThreads, lds, s>>>(a);
@@ -164,6 +173,7 @@ void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t
     if (!gram_hot_lds() || g.hot == 0) {
         lds -= sizeof(double) * (size_t)g.hot;
         g.hot = 0;
+        g.mirror = 0;  // (the mirrored form keeps the hot columns in LDS)
         if (mode == MODE_PLUS) launch_sg<MODE_PLUS, false>(g, grid, lds, s);
         else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, false>(g, grid, lds, s);
         else if (mode == MODE_LSGD) launch_sg3<MODE_LSGD, false, false>(g, grid, lds, s);

@@ -832,7 +832,7 @@ constexpr int kGPart = COCOA_GPART;      // product slots per row (lanes l, l + 
 // SIMD and the two fetch waves on another, 2.97 ms; chain + fetch 0 and
 // loader + fetch 1, 2.85 ms; the memory waves keep a SIMD each.  Four classes
 // (ten waves, a memory wave beside the chain) measured 3.35 ms.
-enum GRole : int { kRChain = 0, kRLoader = 1, kRMem = 2, kRFetch = 2 + kGNC, kRIdle = 2 + 2 * kGNC };
+enum GRole : int { kRChain = 0, kRLoader = 1, kRMem = 2, kRFetch = 2 + kGNC, kRIdle = 2 + 2 * kGNC, kRRelay = 3 + 2 * kGNC };
 #ifndef COCOA_GLAYOUT
 #define COCOA_GLAYOUT kRChain, kRLoader, kRMem, kRMem + 1, kRFetch, kRFetch + 1
 #endif
@@ -861,7 +861,9 @@ struct GLay {                          // one batch's rows of one class, for the
 };
 
 // counters (LDS, release / acquire); kCScat .. kCFetch: one per class
-constexpr int kCChain = 0, kCLoad = 1, kCAbort = 2, kCScat = 3, kCBase = kCScat + kGNC, kCFreed = kCBase + kGNC,
+// kCBase + r: the partial base of column run r (kGramRuns of them: the
+// one-workgroup solver uses r < kGNC, one per class; the mirrored one all four)
+constexpr int kCChain = 0, kCLoad = 1, kCAbort = 2, kCScat = 3, kCBase = kCScat + kGNC, kCFreed = kCBase + kGramRuns,
               kCFetch = kCFreed + kGNC;
 static_assert(kCFetch + kGNC <= 32, "counters");
 
@@ -872,7 +874,7 @@ struct GramSolverLds {
     GRec rec[kGRing * kGB];            // ring: (b % kGRing) * kGB + i
     double coef[kGRing * 2 * kGB];     // c_j, same ring (chain -> memory waves); [kGB, 2 kGB) of a slot stay 0
     GLay lay[kGRing][kGNC];            // same ring (loader -> fetch / memory waves)
-    double base[kGNC][kGSlots];        // partial base_s per class and slot (memory waves -> chain)
+    double base[kGramRuns][kGSlots];   // partial base_s per class (mirrored: per run) and slot (memory waves -> chain)
     double part[kGNC][kGB + 1][kGPart];  // memory wave: row partial sums of a batch's products (+ a sink row)
     alignas(16) double gring[kGGt][kGB][kGW];      // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
     int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
@@ -961,8 +963,13 @@ __device__ __forceinline__ double gram_rule(double u, double aa) {
 //                   the per-class row layouts, up to kGRing batches ahead;
 //   fetch c      -- copy each batch's class-c (column, value) entries into the
 //                   class's LDS sub-ring (LDS DMA), ahead of the gathers.
-template <int MODE, bool HOTLDS, bool PROJ, int XWM>
-__global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArgs a) {
+// MIRROR: two workgroups per partition (grid 2 K), each running the chain and
+// the loader on identical inputs (so both form the same coefficients bit for
+// bit) and the memory / fetch waves of the deltaW columns of its parity h; a
+// seventh wave (relay) copies the other half's partial bases of every batch
+// from xbase into LDS.  Each half thus scatters and gathers half the entries.
+template <int MODE, bool HOTLDS, bool PROJ, int XWM, bool MIRROR = false>
+__global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolverArgs a) {
     constexpr bool XW = XWM == kXwProducer;  // x.w: plan_xw (kXwPlan) or the producer's flags
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramSolverLds& S = *(GramSolverLds*)lds_raw;
@@ -970,32 +977,37 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     double* hotl = (double*)(lds_raw + ((sizeof(GramSolverLds) + 15) & ~(size_t)15));
     const int32_t hot = HOTLDS ? a.hot : 0;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int k = blockIdx.x;
+    const int KP = MIRROR ? (int)(gridDim.x / 2) : (int)gridDim.x;
+    const int k = MIRROR ? (int)(blockIdx.x % (unsigned)KP) : (int)blockIdx.x;
+    const int h = MIRROR ? (int)(blockIdx.x / (unsigned)KP) : 0;  // (same XCD as its pair when K % 8 == 0)
+    constexpr int NRUN = MIRROR ? kGramRuns : kGNC;  // partial bases the chain sums
+    constexpr int NTH = MIRROR ? kGThreads + 64 : kGThreads;
     const int32_t H = a.H, NB = (H + kGB - 1) / kGB;
     int role = kRIdle;
 #pragma unroll
     for (int i = 0; i < kGWaves; ++i)
         if (wv == i) role = kGRoles[i];
+    if (MIRROR && wv == kGWaves) role = kRRelay;
     role = __builtin_amdgcn_readfirstlane(role);
     const int64_t p0 = a.part_ptr[k];
     const int32_t nl = (int32_t)(a.part_ptr[k + 1] - p0);
     const size_t g0 = (size_t)k * H;
     double* dwk = a.dw + (size_t)k * a.d;
     // working alpha of the partition (global), plus a sink at [nl] for the padding steps
-    double* alv = a.alpha_work + p0 + k;
+    double* alv = a.alpha_work + p0 + k + (MIRROR ? h * a.alpha_work_stride : 0);
     const double* gt = a.gt + (size_t)k * a.nbatch * kGB * kGW;
     int* abortf = &S.cnt[kCAbort];
 
     if (MODE != MODE_LSGD) {
-        for (int32_t i = tid; i < nl; i += kGThreads) alv[i] = a.alpha[p0 + i];
+        for (int32_t i = tid; i < nl; i += NTH) alv[i] = a.alpha[p0 + i];
         if (tid == 0) alv[nl] = 0.0;
     }
-    for (int i = tid; i < kGNC * kGSlots; i += kGThreads) (&S.base[0][0])[i] = 0.0;  // batches 0 .. kGNB-1
-    for (int32_t i = tid; i < hot; i += kGThreads) hotl[i] = 0.0;
-    for (int i = tid; i < kGRing * 2 * kGB; i += kGThreads) S.coef[i] = 0.0;  // zero slots: rows past a batch
+    for (int i = tid; i < kGramRuns * kGSlots; i += NTH) (&S.base[0][0])[i] = 0.0;  // batches 0 .. kGNB-1
+    for (int32_t i = tid; i < hot; i += NTH) hotl[i] = 0.0;
+    for (int i = tid; i < kGRing * 2 * kGB; i += NTH) S.coef[i] = 0.0;  // zero slots: rows past a batch
     if (tid < 32) S.cnt[tid] = 0;
     __syncthreads();
-    if (tid < kGNC) S.cnt[kCBase + tid] = kGNB;
+    if (tid < kGramRuns) S.cnt[kCBase + tid] = kGNB;
     __syncthreads();
     uint64_t wait_cycles = 0;
     uint64_t* pw = a.prof ? &wait_cycles : nullptr;
@@ -1010,7 +1022,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         // the step's inputs one batch ahead (registers)
         const int i = lane & (kGB - 1);
         int32_t xr = nl, xz = 0;
-        int32_t xzc[kGNC - 1];  // ends of the class runs 0 .. kGNC-2 in the row
+        int32_t xzc[kGramRuns - 1];  // ends of the column runs 0 .. 2 in the row
         double xy = 0.0, xq = 0.0, xxw = 0.0;
         int64_t xbeg = 0;
         double ls = 1.0;   // MODE_LSGD: s before the batch (SGD.scala:119-120), wave-uniform
@@ -1067,7 +1079,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             xr = nl;
             xz = 0;
 #pragma unroll
-            for (int c = 0; c < kGNC - 1; ++c) xzc[c] = 0;
+            for (int c = 0; c < kGramRuns - 1; ++c) xzc[c] = 0;
             xy = xq = xxw = 0.0;
             xbeg = 0;
             if (lane < kGB && j < H) {
@@ -1082,7 +1094,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 xbeg = a.plan_beg[g0 + j];
                 xz = a.plan_z[g0 + j];
 #pragma unroll
-                for (int c = 0; c < kGNC - 1; ++c) xzc[c] = a.plan_zc ? a.plan_zc[4 * (g0 + j) + c] : xz;
+                for (int c = 0; c < kGramRuns - 1; ++c) xzc[c] = a.plan_zc ? a.plan_zc[4 * (g0 + j) + c] : xz;
             }
         };
         load(0);
@@ -1104,11 +1116,20 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 const int32_t j = b * kGB + i;
                 const bool valid = lane < kGB && j < H;
                 const int32_t r = xr, z = xz;
-                int32_t ze[kGNC + 1];  // class c: entries [beg + ze[c], beg + ze[c+1])
-                ze[0] = 0;
+                // class c: entries [beg + ze[c], beg + ze[c+1]) -- runs 2c, 2c+1, or
+                // (mirrored) run 2c + h
+                int32_t zr[kGramRuns + 1];
+                zr[0] = 0;
 #pragma unroll
-                for (int c = 0; c < kGNC - 1; ++c) ze[c + 1] = xzc[c];
-                ze[kGNC] = z;
+                for (int c = 0; c < kGramRuns - 1; ++c) zr[c + 1] = xzc[c];
+                zr[kGramRuns] = z;
+                int32_t ze[kGNC + 1], zb[kGNC];
+#pragma unroll
+                for (int c = 0; c < kGNC; ++c) {
+                    zb[c] = MIRROR ? (h ? zr[2 * c + 1] : zr[2 * c]) : zr[2 * c];
+                    ze[c + 1] = MIRROR ? (h ? zr[2 * c + 2] : zr[2 * c + 1]) : zr[2 * c + 2];
+                }
+                ze[0] = 0;
                 if (XW && xw_miss) xw_inline();  // (wave-uniform)
                 const double y = xy, q = xq, xw = xxw;
                 const int64_t beg = xbeg;
@@ -1119,7 +1140,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 int32_t inc[kGNC], T[kGNC], nu[kGNC];
 #pragma unroll
                 for (int c = 0; c < kGNC; ++c) {
-                    const int32_t zc = ze[c + 1] - ze[c];
+                    const int32_t zc = ze[c + 1] - zb[c];
                     inc[c] = wave_incl_scan(lane < kGB ? zc : 0);
                     T[c] = __shfl(inc[c], kGB - 1, 64);
                     nu[c] = (T[c] + 63) >> 6;
@@ -1191,7 +1212,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     GLay& L = S.lay[b % kGRing][c];
                     if (lane < kGB) {
                         L.sx[lane + 1] = inc[c];
-                        L.sb[lane] = beg + ze[c];
+                        L.sb[lane] = beg + zb[c];
                     }
                     if (lane == 0) {
                         L.sx[0] = 0;
@@ -1253,6 +1274,18 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
     } else if (role >= kRMem && role < kRFetch) {
         // ------------------------------------------------------- memory --
         const int c = role - kRMem;  // this wave's column class
+        const int bslot = MIRROR ? 2 * c + h : c;  // its partial base: class c, or (mirrored) run 2c + h
+        // (mirrored) hand batch x's partial base to the other half: 16 doubles as 32
+        // tagged 8-byte granules, sc1 stores (no drain, no flag: the tag is the flag)
+        auto publish = [&](int32_t x) {
+            if (!MIRROR || lane >= 2 * kGB) return;
+            const double v = S.base[bslot][(x % kGNB) * kGB + (lane >> 1)];
+            const uint64_t bits = (uint64_t)__double_as_longlong(v);
+            const uint32_t tag = ((uint32_t)(a.xtag_epoch & 0xFFF) << 20) | (uint32_t)(x + 1);
+            const uint64_t gr = ((uint64_t)tag << 32) | ((lane & 1) ? (bits >> 32) : (bits & 0xFFFFFFFFull));
+            uint64_t* gp = a.xbase + (((size_t)k * kGramRuns + bslot) * kXbR + (x % kXbR)) * (2 * kGB) + lane;
+            __hip_atomic_store(gp, gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
         const bool bases = MODE != MODE_MBCD;
         double hv[kGMaxU], dw[kGMaxU];  // in-flight gathers: staged value (x hot deltaW), loaded deltaW (or 1)
         uint32_t hrow[(kGMaxU + 5) / 6];  //   and their rows (5 bits per unit, 31 = no entry)
@@ -1359,9 +1392,10 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 for (int t = 0; t < kGPart / 4; ++t) s4 += part[rr][qq + t];
                 s4 += dpp_row_d<0xB1>(s4);  // quad_perm [1,0,3,2]
                 s4 += dpp_row_d<0x4E>(s4);  // quad_perm [2,3,0,1]
-                if ((lane & 3) == 0) S.base[c][(xin % kGNB) * kGB + rr] = s4;
+                if ((lane & 3) == 0) S.base[bslot][(xin % kGNB) * kGB + rr] = s4;
                 wave_lds_sync();
-                if (lane == 0) lds_release(&S.cnt[kCBase + c], xin + 1);
+                if (lane == 0) lds_release(&S.cnt[kCBase + bslot], xin + 1);
+                publish(xin);
                 xin = -1;
             }
             stamp(1);
@@ -1421,7 +1455,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                     xnu = nu;
                 } else {
                     // too long to stage: gathered and summed here
-                    double* bs = S.base[c] + (x % kGNB) * kGB;
+                    double* bs = S.base[bslot] + (x % kGNB) * kGB;
                     for (int i = 0; i < kGB; ++i) {
                         const int32_t z = L.sx[i + 1] - L.sx[i];
                         const int64_t rb = L.sb[i];
@@ -1431,7 +1465,8 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                         if (lane == 0) bs[i] = t;
                     }
                     wave_lds_sync();
-                    if (lane == 0) lds_release(&S.cnt[kCBase + c], x + 1);
+                    if (lane == 0) lds_release(&S.cnt[kCBase + bslot], x + 1);
+                    publish(x);
                 }
             }
             stamp(2);
@@ -1439,6 +1474,49 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         vm_drain();  // the last atomics land before the kernel ends
         if (a.prof && lane == 0)
             for (int i = 0; i < 4; ++i) a.prof[(size_t)k * kProfStride + 48 + 4 * c + i] = ph[i];
+    } else if (MIRROR && role == kRRelay) {
+        // -------------------------------------------------------- relay --
+        // the other half's partial bases (its runs hp and 2 + hp) of every batch
+        // x >= kGNB, from its tagged granules into this half's LDS
+        if (MODE != MODE_MBCD) {
+            const int hp = 1 - h;
+            const int run = 2 * (lane >> 5) + hp;  // lanes 0-31: run hp, 32-63: run 2 + hp
+            const int row = (lane >> 1) & (kGB - 1), half = lane & 1;
+            const uint32_t thi = (uint32_t)(a.xtag_epoch & 0xFFF) << 20;
+            for (int32_t x = kGNB; x < NB; ++x) {
+                // base slot x % kGNB held batch x - kGNB: the chain is done with it
+                if (!wait_ge(&S.cnt[kCChain], x - kGNB + 1, abortf, a.status, pw)) break;
+                uint64_t* gp = a.xbase + (((size_t)k * kGramRuns + run) * kXbR + (x % kXbR)) * (2 * kGB) + (lane & 31);
+                const uint32_t tag = thi | (uint32_t)(x + 1);
+                uint64_t gv = 0;
+                bool ok = true;
+                const uint64_t t0 = pw ? __builtin_readcyclecounter() : 0;
+                for (uint32_t it = 0;; ++it) {  // sc1 polls of the 64 granules until every tag matches
+                    gv = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all((uint32_t)(gv >> 32) == tag)) break;
+                    if (__hip_atomic_load(abortf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                        ok = false;
+                        break;
+                    }
+                    if (it > (1u << 24)) {
+                        __hip_atomic_store(abortf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (lane == 0) __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (pw) *pw += __builtin_readcyclecounter() - t0;
+                if (!ok) break;
+                const uint32_t mine = (uint32_t)gv, other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+                if (half == 0) S.base[run][(x % kGNB) * kGB + row] = __hiloint2double((int)other, (int)mine);
+                wave_lds_sync();
+                if (lane == 0) {
+                    lds_release(&S.cnt[kCBase + hp], x + 1);
+                    lds_release(&S.cnt[kCBase + 2 + hp], x + 1);
+                }
+            }
+        }
     } else if (role == kRChain) {
         // -------------------------------------------------------- chain --
         // lane = window slot (step mod kGW): sdot = base + Gram corrections
@@ -1462,7 +1540,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             const bool mine = lane / kGB == q4;
             if (MODE != MODE_MBCD) {
 #pragma unroll
-                for (int c = 0; c < kGNC; ++c)
+                for (int c = 0; c < NRUN; ++c)
                     if (!wait_ge(&S.cnt[kCBase + c], g + 1, abortf, a.status, pw)) return false;
                 if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw)) return false;
             } else if (!wait_ge(&S.cnt[kCLoad], min(g + kGNB + 1, NB), abortf, a.status, pw)) {
@@ -1478,9 +1556,10 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
                 aissue = alv[(mine && g4 < NB) ? R4.r : nl];  // one load for every lane (the sink otherwise)
             }
             if (mine) {
+                // (mirrored: runs in order 0..3 on both halves, so both chains add alike)
                 double bsum = S.base[0][lane];
 #pragma unroll
-                for (int c = 1; c < kGNC; ++c) bsum += S.base[c][lane];
+                for (int c = 1; c < NRUN; ++c) bsum += S.base[c][lane];
                 acc += bsum;
             }
             double gcur[kGB];
@@ -1584,7 +1663,7 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
             if (g + 1 < NB && !batch(g + 1, aB, aA)) break;
         }
     }
-    if (a.prof && lane == 0) {
+    if (a.prof && lane == 0 && h == 0 && wv < kGWaves) {
         uint64_t* pr = a.prof + (size_t)k * kProfStride + wv * 4;  // [k][64]: waves at 4 wv, memory phases at 48 + 4 c
         pr[0] = wait_cycles;
         pr[1] = __builtin_readcyclecounter() - t_start;
@@ -1594,18 +1673,27 @@ __global__ __launch_bounds__(kGThreads, 1) void solver_gram_kernel(GramSolverArg
         // deltaW = w - wInit = s (keep wInit + v) - wInit (SGD.scala:133), the slice
         // holding v (L2: read past L1, like the gathers)
         const double sH = S.lsgd_s, f = S.lsgd_keep ? sH - 1.0 : -1.0;
-        for (int64_t j = tid; j < a.d; j += kGThreads) {
+        for (int64_t j = tid; j < a.d; j += NTH) {
             const double v = (HOTLDS && j < hot) ? hotl[j] : dw_load(dwk + j);
             dwk[j] = fma(sH, v, f * a.w[j]);
         }
         return;
     }
-    for (int32_t i = tid; i < hot; i += kGThreads) dwk[i] = hotl[i];  // the slice is zero there: plain stores
+    if (!MIRROR) {
+        for (int32_t i = tid; i < hot; i += NTH) dwk[i] = hotl[i];  // the slice is zero there: plain stores
+    } else {
+        // this half's columns (parity h) only, write-through: the other half's
+        // workgroup writes the interleaved words of the same lines, maybe from
+        // another XCD's L2
+        for (int32_t i = 2 * tid + h; i < hot; i += 2 * NTH)
+            __hip_atomic_store(dwk + i, hotl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (MIRROR && h != 0) return;  // alpha: the first half's (both hold the same)
     // alpha = alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101, MinibatchCD.scala:127-128)
     if (a.raw_alpha) {
-        for (int32_t i = tid; i < nl; i += kGThreads) a.alpha[p0 + i] = alv[i];
+        for (int32_t i = tid; i < nl; i += NTH) a.alpha[p0 + i] = alv[i];
     } else {
-        for (int32_t i = tid; i < nl; i += kGThreads) {
+        for (int32_t i = tid; i < nl; i += NTH) {
             const double old = a.alpha[p0 + i];
             a.alpha[p0 + i] = old + ((alv[i] - old) * a.scaling);
         }
