@@ -823,6 +823,9 @@ constexpr int kGOCol = 0, kGOLo = 256, kGOHi = 512, kGORow = 768;  // its fields
 constexpr int kGMaxU = kGSub / 4;        // units of one class of a staged batch (4 live batches per
                                          // sub-ring); larger batches go direct
 constexpr int kGGt = 4;                  // Gram-row ring (batches)
+#ifndef COCOA_EARLY_RELEASE
+#define COCOA_EARLY_RELEASE 0  // 1: memory waves free a staged batch's slots before its atomics (r06n: solver 2.34 -> 2.39 ms, not kept)
+#endif
 #ifndef COCOA_GPART
 #define COCOA_GPART 16  // (32: 1.4% slower, 544 fewer LDS-resident deltaW columns; r03 A/B)
 #endif
@@ -1009,7 +1012,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     __syncthreads();
     if (tid < kGramRuns) S.cnt[kCBase + tid] = kGNB;
     __syncthreads();
-    uint64_t wait_cycles = 0;
+    uint64_t wait_cycles = 0, wait_base_local = 0, wait_base_remote = 0;  // (diagnostics: the chain's base waits)
     uint64_t* pw = a.prof ? &wait_cycles : nullptr;
     const uint64_t t_start = a.prof ? __builtin_readcyclecounter() : 0;
 
@@ -1346,6 +1349,14 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                     }
                 }
                 stamp(3);
+                // staged: the ring entries and coefficients are in registers now, so the
+                // slots go back before the atomics (their release would otherwise also
+                // wait for this wave's LDS atomics into the hot columns)
+                wave_lds_sync();
+                if (COCOA_EARLY_RELEASE && pos >= 0 && lane == 0) {
+                    lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
+                    lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                }
                 if (bases) vm_drain();  // the gathers of batch b+kGNB-1 have read the slice (MbCD: no gathers)
                 stamp(0);
                 if (pos >= 0) {
@@ -1361,10 +1372,12 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                         for (int32_t e = lane; e < z; e += 64) dw_add(a.col[rb + e], a.val[rb + e] * cv);
                     }
                 }
-                wave_lds_sync();
-                if (lane == 0) {
-                    lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
-                    if (pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                if (!COCOA_EARLY_RELEASE || pos < 0) {  // (the direct path read the layout and coefficients until here)
+                    wave_lds_sync();
+                    if (lane == 0) {
+                        lds_release(&S.cnt[kCScat + c], b + 1);
+                        if (!COCOA_EARLY_RELEASE && pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                    }
                 }
             }
             // 1. products of the gathers in flight -> this class's part of the base of
@@ -1541,7 +1554,9 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             if (MODE != MODE_MBCD) {
 #pragma unroll
                 for (int c = 0; c < NRUN; ++c)
-                    if (!wait_ge(&S.cnt[kCBase + c], g + 1, abortf, a.status, pw)) return false;
+                    if (!wait_ge(&S.cnt[kCBase + c], g + 1, abortf, a.status,
+                                 !pw ? nullptr : (MIRROR && (c & 1) != h) ? &wait_base_remote : &wait_base_local))
+                        return false;
                 if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw)) return false;
             } else if (!wait_ge(&S.cnt[kCLoad], min(g + kGNB + 1, NB), abortf, a.status, pw)) {
                 return false;
@@ -1665,7 +1680,11 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     }
     if (a.prof && lane == 0 && h == 0 && wv < kGWaves) {
         uint64_t* pr = a.prof + (size_t)k * kProfStride + wv * 4;  // [k][64]: waves at 4 wv, memory phases at 48 + 4 c
-        pr[0] = wait_cycles;
+        pr[0] = wait_cycles + (role == kRChain ? wait_base_local + wait_base_remote : 0);
+        if (role == kRChain) {
+            pr[2] = wait_base_local;
+            pr[3] = wait_base_remote;
+        }
         pr[1] = __builtin_readcyclecounter() - t_start;
     }
     __syncthreads();

@@ -49,6 +49,7 @@ def main():
     # tag -> (substring the kernel name must hold, substrings it must not hold)
     tags = (("solver_chain", "solver_kernel<", ()), ("solver_gram", "solver_gram_kernel", ()),
             ("solver_dense", "dense_solver_kernel", ()), ("gram", "gram_kernel", ("solver_gram",)),
+            ("gram_seq", "gram_seq_kernel", ()), ("gram_list", "gram_list_kernel", ()),
             ("eval", "eval_stream_kernel", ()), ("eval_dense", "eval_dense_kernel", ()),
             ("plan", "plan_kernel", ()), ("fold", "fold_kernel", ("compact",)),
             ("fold_compact", "fold_compact_kernel", ()), ("fold_blocks", "fold_blocks_kernel", ()),
@@ -57,6 +58,8 @@ def main():
         names = sorted({k for (k, c) in f if needle in k and not any(b in k for b in bad)})
         if not names:
             continue
+        # the instantiation launched most (round 1's x.w-producer form runs once)
+        names.sort(key=lambda k: -pick(f, k, "FETCH_SIZE")[1])
         fe, n = pick(f, names[0], "FETCH_SIZE")
         wr, _ = pick(w, names[0], "WRITE_SIZE")
         if fe is None or wr is None:

@@ -44,6 +44,8 @@ def main():
                          "wait_frac": float(raw[:, i, 0].sum() / max(raw[:, i, 1].sum(), 1))}
                      for i, r in enumerate(roles)},
            "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
+           "chain_base_wait_frac": {"local": float(raw[:, 0, 2].sum() / max(raw[:, 0, 1].sum(), 1)),
+                                    "remote": float(raw[:, 0, 3].sum() / max(raw[:, 0, 1].sum(), 1))},
            "memory_phases_cyc_per_batch": {
                "memory%d" % c: dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
                                         (full[:, 48 + 4 * c:52 + 4 * c].mean(axis=0) / nb).tolist()))
