@@ -256,6 +256,7 @@ struct cocoa_ctx {
     DevBuf gram_fb[2];
     int gram_chunks = 0;  // > 0: Gram rows by gram_seq_kernel, this many batch runs per partition
     bool gram_mirror = false;  // the Gram solver as two workgroups per partition (solver_gram.h MIRROR)
+    int32_t hot_split = 0;     // hot / cold run boundary of the fast-mode rows (COCOA_HOTRUNS)
     DevBuf xbase;              //   their partial-base exchange ([K][4][kXbR][16][2] tagged granules)
     int32_t xtag_epoch = 0;    //   launch counter in the granule tags
     hipStream_t gstream = nullptr;
@@ -891,7 +892,15 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     // LDS-resident columns vs the rest, or the columns holding the first half of
     // the entries vs the rest -- measured 3.93 / 2.97 ms against 2.70: the first
     // class's fetch and memory waves carry most of the units; r03 A/B)
-    auto class_of = [&](int32_t c) -> int { return c % kGramRuns; };
+    // (COCOA_HOTRUNS: parity, then the LDS-resident columns of the Gram solver
+    // [0, hot_split) before the rest; COCOA_HOT_SPLIT=j moves the boundary down)
+    int32_t hsplit = -1;
+    if (COCOA_HOTRUNS) {
+        gram_solver_lds(num_features, &hsplit);
+        if (const char* e = std::getenv("COCOA_HOT_SPLIT")) hsplit = std::max(0, std::min(hsplit, std::atoi(e)));
+    }
+    ctx->hot_split = std::max(hsplit, 0);
+    auto class_of = [&](int32_t c) -> int { return hsplit >= 0 ? 2 * (c & 1) + (c >= hsplit ? 1 : 0) : c % kGramRuns; };
     if (split_classes) {
         pval.resize((size_t)nnz);
         zcv.resize((size_t)std::max<int64_t>(n_rows, 1) * 4);
@@ -1656,6 +1665,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.lambda = c->P.lambda;
             g.t0 = lsgd_t0;
             g.alpha_work_stride = c->tr.n + K;
+            g.hot_split = c->hot_split;
             g.mirror = c->gram_mirror ? 1 : 0;
             g.xbase = c->xbase.as<uint64_t>();
             if (c->gram_mirror) c->xtag_epoch = (c->xtag_epoch % 4095) + 1;  // 1..4095 (12 tag bits, never 0)

@@ -27,7 +27,16 @@ constexpr int kWave = 64;
 #endif
 constexpr int kGramClasses = COCOA_GNC;
 static_assert(kGramClasses == 2, "column classes per workgroup");
-constexpr int kGramRuns = 4;        // column runs of a fast-mode row (c % 4)
+constexpr int kGramRuns = 4;        // column runs of a fast-mode row
+// COCOA_HOTRUNS=1: run = 2 (c & 1) + (c >= hot_split) -- even hot, even cold, odd
+// hot, odd cold -- so a class (one per parity) is its hot run then its cold run,
+// and the mirrored solver's half h gives its two memory waves the hot and the
+// cold run of parity h (LDS-only and global-only code).  0: run = c % 4.
+// (r06p, one box: the hot / cold classes 2.85 ms against 2.67 for c % 4 -- the
+// hot-only wave carries ~70% of the half's entries; COCOA_HOT_SPLIT lowers it)
+#ifndef COCOA_HOTRUNS
+#define COCOA_HOTRUNS 0
+#endif
 constexpr int kProfStride = 64;     // solver profile words per partition (diagnostics)
 constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
 #ifndef COCOA_REG_CHUNKS
@@ -193,6 +202,10 @@ struct GramSolverArgs {
     int32_t xtag_epoch;
     uint64_t* xbase;          // [K][kGramRuns][kXbR][kGB][2]
     int64_t alpha_work_stride;  // n + K (mirror)
+    // the hot / cold run boundary of the rows' layout (COCOA_HOTRUNS, cocoa_set_train);
+    // the mirrored solver specialises its memory waves when it equals hot
+    int32_t hot_split;
+    int32_t hot_split_pad;
 };
 constexpr int kXbR = 8;     // xbase ring (batches)
 

@@ -170,10 +170,12 @@ void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t
     }
     if (const char* e = getenv("COCOA_GRAM_DIAG")) g.diag = atoi(e);
 #endif
+    if (g.hot_split > g.hot) g.hot_split = 0;  // (a hot-only class must be LDS-resident)
     if (!gram_hot_lds() || g.hot == 0) {
         lds -= sizeof(double) * (size_t)g.hot;
         g.hot = 0;
         g.mirror = 0;  // (the mirrored form keeps the hot columns in LDS)
+        g.hot_split = 0;
         if (mode == MODE_PLUS) launch_sg<MODE_PLUS, false>(g, grid, lds, s);
         else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, false>(g, grid, lds, s);
         else if (mode == MODE_LSGD) launch_sg3<MODE_LSGD, false, false>(g, grid, lds, s);

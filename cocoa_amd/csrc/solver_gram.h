@@ -64,6 +64,7 @@
 // exactly 0 (step 1 of round 1) drops wInit: keep = 0, s = 1.  The epilogue
 // writes deltaW = w - wInit = s keep wInit + s v - wInit (SGD.scala:133).
 #pragma once
+#include <type_traits>
 #include "kernels.h"
 #include "wave.h"
 
@@ -908,6 +909,10 @@ __device__ __forceinline__ void gram_row_consts(const GramSolverArgs& a, double 
     Y = y * a.inv_lam_n;
 }
 
+// the column run of class c of the mirrored solver's half h (kernels.h COCOA_HOTRUNS):
+// half h owns the columns of parity h in both layouts
+__device__ __forceinline__ int gram_mirror_run(int c, int h) { return COCOA_HOTRUNS ? 2 * h + c : 2 * c + h; }
+
 // packed position q of a batch's rows -> row: largest i with excl[i] <= q
 __device__ __forceinline__ int gram_owner(const int32_t* excl, int32_t q) {
     int lo = 0;
@@ -1129,8 +1134,9 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 int32_t ze[kGNC + 1], zb[kGNC];
 #pragma unroll
                 for (int c = 0; c < kGNC; ++c) {
-                    zb[c] = MIRROR ? (h ? zr[2 * c + 1] : zr[2 * c]) : zr[2 * c];
-                    ze[c + 1] = MIRROR ? (h ? zr[2 * c + 2] : zr[2 * c + 1]) : zr[2 * c + 2];
+                    const int r = gram_mirror_run(c, h);
+                    zb[c] = MIRROR ? zr[r] : zr[2 * c];
+                    ze[c + 1] = MIRROR ? zr[r + 1] : zr[2 * c + 2];
                 }
                 ze[0] = 0;
                 if (XW && xw_miss) xw_inline();  // (wave-uniform)
@@ -1277,7 +1283,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     } else if (role >= kRMem && role < kRFetch) {
         // ------------------------------------------------------- memory --
         const int c = role - kRMem;  // this wave's column class
-        const int bslot = MIRROR ? 2 * c + h : c;  // its partial base: class c, or (mirrored) run 2c + h
+        const int bslot = MIRROR ? gram_mirror_run(c, h) : c;  // its partial base: class c, or (mirrored) its run
         // (mirrored) hand batch x's partial base to the other half: 16 doubles as 32
         // tagged 8-byte granules, sc1 stores (no drain, no flag: the tag is the flag)
         auto publish = [&](int32_t x) {
@@ -1295,11 +1301,6 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         int32_t xin = -1;               // batch whose gathers are in flight
         int32_t xnu = 0;                //   and its 64-entry units
         double(*part)[kGPart] = S.part[c];
-        auto dw_add = [&](int32_t col, double v) {
-            if (HOTLDS && col < hot) __hip_atomic_fetch_add(hotl + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else unsafeAtomicAdd(dwk + col, v);
-        };
-        auto dw_get = [&](int32_t col) { return (HOTLDS && col < hot) ? hotl[col] : dw_load(dwk + col); };
         auto fetched = [&](int32_t x) { return wait_ge(&S.cnt[kCFetch + c], x + 1, abortf, a.status, pw); };
         uint64_t ph[4] = {0, 0, 0, 0};
         uint64_t tph = 0;
@@ -1310,180 +1311,211 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 tph = t;
             }
         };
-        for (int32_t b = 0; b < NB; ++b) {
-            if (!wait_ge(&S.cnt[kCChain], b + 1, abortf, a.status, pw)) break;  // the chain finished batch b
-            if (a.prof) tph = __builtin_readcyclecounter();
-            // Scatter of batch b first, its LDS reads before the drain: the ring entries
-            // and coefficients of b are read into registers while the gathers of batch
-            // b+3 are still in flight; the drain then only orders those gathers before
-            // b's atomics (the per-column order of the slice), and the products of b+3
-            // are formed behind the atomics.
-            {
-                const GLay& L = S.lay[b % kGRing][c];
-                const double* cf = S.coef + (b % kGRing) * (2 * kGB);
-                const int32_t pos = L.pos, nu = L.nu;
-                int32_t scl[kGMaxU];
-                double sp[kGMaxU];
-                if (pos >= 0) {
-                    if (!fetched(b)) break;
-#pragma unroll
-                    for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
-                        if (u0 < nu) {
-                            int rw[4];
-                            double vl[4];
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                uint32_t r8;
-                                ring_get(S, ring_unit(c, pos, u0 + t), lane, scl[u0 + t], vl[t], r8);
-                                rw[t] = r8 | gram_pad(u0 + t, nu);
-                            }
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                // a lane past the batch (row 0xFF) reads a zero slot; its ring
-                                // entry was never written, so it is dropped by the coefficient
-                                const double cc = cf[rw[t] & (2 * kGB - 1)];
-                                sp[u0 + t] = vl[t] * cc;
-                                if (cc == 0.0) scl[u0 + t] = -1;
-                            }
-                        }
-                    }
-                }
-                stamp(3);
-                // staged: the ring entries and coefficients are in registers now, so the
-                // slots go back before the atomics (their release would otherwise also
-                // wait for this wave's LDS atomics into the hot columns)
-                wave_lds_sync();
-                if (COCOA_EARLY_RELEASE && pos >= 0 && lane == 0) {
-                    lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
-                    lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
-                }
-                if (bases) vm_drain();  // the gathers of batch b+kGNB-1 have read the slice (MbCD: no gathers)
-                stamp(0);
-                if (pos >= 0) {
-#pragma unroll
-                    for (int u = 0; u < kGMaxU; ++u)
-                        if (u < nu && scl[u] >= 0 && !(COCOA_DIAG_ON && (a.diag & 1))) dw_add(scl[u], sp[u]);
-                } else {
-                    for (int i = 0; i < kGB; ++i) {
-                        const double cv = cf[i];
-                        if (cv == 0.0) continue;
-                        const int32_t z = L.sx[i + 1] - L.sx[i];
-                        const int64_t rb = L.sb[i];
-                        for (int32_t e = lane; e < z; e += 64) dw_add(a.col[rb + e], a.val[rb + e] * cv);
-                    }
-                }
-                if (!COCOA_EARLY_RELEASE || pos < 0) {  // (the direct path read the layout and coefficients until here)
-                    wave_lds_sync();
-                    if (lane == 0) {
-                        lds_release(&S.cnt[kCScat + c], b + 1);
-                        if (!COCOA_EARLY_RELEASE && pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
-                    }
-                }
-            }
-            // 1. products of the gathers in flight -> this class's part of the base of
-            //    batch xin.  Each unit's product goes to (its row, lane mod 32) with a
-            //    fire-and-forget LDS add (lanes l and l + 32 share a slot: different
-            //    LDS lane groups, no conflict); 4 lanes per row add the slots up.
-            if (xin >= 0) {
-                if (lane < kGPart) {
-#pragma unroll
-                    for (int i = 0; i < kGB; ++i) part[i][lane] = 0.0;
-                }
-                wave_lds_sync();
-#pragma unroll
-                for (int u = 0; u < kGMaxU; ++u) {
-                    if (u < xnu) {
-                        const int row = min((int)((hrow[u / 6] >> (5 * (u % 6))) & 31u), kGB);  // 31: no entry
-                        __hip_atomic_fetch_add(&part[row][lane & (kGPart - 1)], hv[u] * dw[u], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-                wave_lds_sync();
-                const int rr = lane >> 2, qq = (lane & 3) * (kGPart / 4);
-                double s4 = 0.0;
-#pragma unroll
-                for (int t = 0; t < kGPart / 4; ++t) s4 += part[rr][qq + t];
-                s4 += dpp_row_d<0xB1>(s4);  // quad_perm [1,0,3,2]
-                s4 += dpp_row_d<0x4E>(s4);  // quad_perm [2,3,0,1]
-                if ((lane & 3) == 0) S.base[bslot][(xin % kGNB) * kGB + rr] = s4;
-                wave_lds_sync();
-                if (lane == 0) lds_release(&S.cnt[kCBase + bslot], xin + 1);
-                publish(xin);
-                xin = -1;
-            }
-            stamp(1);
-            // 3. gathers of batch x = b + kGNB on this class's columns: they see batch
-            //    b's updates (issued above, same wave, same addresses) and nothing later
-            //    (the next atomics go out after step 1 has consumed these loads)
-            const int32_t x = b + kGNB;
-            if (bases && x < NB) {
-                const GLay& L = S.lay[x % kGRing][c];
-                const int32_t pos = L.pos, nu = L.nu;
-                if (pos >= 0) {
-                    if (!fetched(x)) break;
-#pragma unroll
-                    for (int w = 0; w < (kGMaxU + 5) / 6; ++w) hrow[w] = 0xFFFFFFFFu;  // units past nu: never read
-                    // groups of 4 units (a group past the batch is skipped whole)
-#pragma unroll
-                    for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
-                        if (u0 < nu) {
-                            int rw[4];
-                            int32_t cl[4];
-                            double vl[4];
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                uint32_t r8;
-                                ring_get(S, ring_unit(c, pos, u0 + t), lane, cl[t], vl[t], r8);
-                                rw[t] = r8 | gram_pad(u0 + t, nu);
-                            }
-                            double hx[4];
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                const int u = u0 + t;
-                                const int32_t cc = rw[t] < kGB ? cl[t] : -1;
-                                // a hot (LDS) or empty lane loads the constant 1 -- one register
-                                // never mixes a global load with an LDS read (that would serialise)
-                                if (HOTLDS) {
-                                    if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(cc >= hot ? dwk + cc : &g_gram_one);
-                                    hx[t] = hotl[(cc >= 0 && cc < hot) ? cc : 0];
-                                } else if (!(COCOA_DIAG_ON && (a.diag & 2))) {
-                                    // a lane past the batch loads column 0: its product goes to the sink row
-                                    dw[u] = dw_load(dwk + (cc >= 0 ? cc : 0));
+        // KIND 0: a class mixing LDS-resident and slice columns; 1 / 2: the mirrored
+        // half's hot-only (LDS) / cold-only (slice) class of the COCOA_HOTRUNS layout
+        auto mem_loop = [&](auto kind_c) {
+            constexpr int KIND = decltype(kind_c)::value;
+            auto dw_addk = [&](int32_t col, double v) {
+                if (KIND == 1 || (KIND == 0 && HOTLDS && col < hot))
+                    __hip_atomic_fetch_add(hotl + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    unsafeAtomicAdd(dwk + col, v);
+            };
+            auto dw_getk = [&](int32_t col) {
+                return (KIND == 1 || (KIND == 0 && HOTLDS && col < hot)) ? hotl[col] : dw_load(dwk + col);
+            };
+            for (int32_t b = 0; b < NB; ++b) {
+                if (!wait_ge(&S.cnt[kCChain], b + 1, abortf, a.status, pw)) break;  // the chain finished batch b
+                if (a.prof) tph = __builtin_readcyclecounter();
+                // Scatter of batch b first, its LDS reads before the drain: the ring entries
+                // and coefficients of b are read into registers while the gathers of batch
+                // b+3 are still in flight; the drain then only orders those gathers before
+                // b's atomics (the per-column order of the slice), and the products of b+3
+                // are formed behind the atomics.
+                {
+                    const GLay& L = S.lay[b % kGRing][c];
+                    const double* cf = S.coef + (b % kGRing) * (2 * kGB);
+                    const int32_t pos = L.pos, nu = L.nu;
+                    int32_t scl[kGMaxU];
+                    double sp[kGMaxU];
+                    if (pos >= 0) {
+                        if (!fetched(b)) break;
+    #pragma unroll
+                        for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
+                            if (u0 < nu) {
+                                int rw[4];
+                                double vl[4];
+    #pragma unroll
+                                for (int t = 0; t < 4; ++t) {
+                                    uint32_t r8;
+                                    ring_get(S, ring_unit(c, pos, u0 + t), lane, scl[u0 + t], vl[t], r8);
+                                    rw[t] = r8 | gram_pad(u0 + t, nu);
+                                }
+    #pragma unroll
+                                for (int t = 0; t < 4; ++t) {
+                                    // a lane past the batch (row 0xFF) reads a zero slot; its ring
+                                    // entry was never written, so it is dropped by the coefficient
+                                    const double cc = cf[rw[t] & (2 * kGB - 1)];
+                                    sp[u0 + t] = vl[t] * cc;
+                                    if (cc == 0.0) scl[u0 + t] = -1;
                                 }
                             }
-                            __builtin_amdgcn_sched_barrier(0);  // all reads of the group out before the products
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                const int u = u0 + t;
-                                const bool ok = rw[t] < kGB;
-                                if (HOTLDS)
-                                    hv[u] = ok ? ((cl[t] < hot) ? vl[t] * hx[t] : vl[t]) : 0.0;
-                                else
-                                    hv[u] = vl[t];  // past the batch: any value, summed into the sink row
-                                hrow[u / 6] = (hrow[u / 6] & ~(31u << (5 * (u % 6)))) | ((uint32_t)(ok ? rw[t] : 31) << (5 * (u % 6)));
-                            }
                         }
                     }
-                    xin = x;
-                    xnu = nu;
-                } else {
-                    // too long to stage: gathered and summed here
-                    double* bs = S.base[bslot] + (x % kGNB) * kGB;
-                    for (int i = 0; i < kGB; ++i) {
-                        const int32_t z = L.sx[i + 1] - L.sx[i];
-                        const int64_t rb = L.sb[i];
-                        double acc = 0.0;
-                        for (int32_t e = lane; e < z; e += 64) acc = fma(a.val[rb + e], dw_get(a.col[rb + e]), acc);
-                        const double t = wave_sum(acc);
-                        if (lane == 0) bs[i] = t;
+                    stamp(3);
+                    // staged: the ring entries and coefficients are in registers now, so the
+                    // slots go back before the atomics (their release would otherwise also
+                    // wait for this wave's LDS atomics into the hot columns)
+                    wave_lds_sync();
+                    if (COCOA_EARLY_RELEASE && pos >= 0 && lane == 0) {
+                        lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
+                        lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                    }
+                    if (bases) vm_drain();  // the gathers of batch b+kGNB-1 have read the slice (MbCD: no gathers)
+                    stamp(0);
+                    if (pos >= 0) {
+    #pragma unroll
+                        for (int u = 0; u < kGMaxU; ++u)
+                            if (u < nu && scl[u] >= 0 && !(COCOA_DIAG_ON && (a.diag & 1))) dw_addk(scl[u], sp[u]);
+                    } else {
+                        for (int i = 0; i < kGB; ++i) {
+                            const double cv = cf[i];
+                            if (cv == 0.0) continue;
+                            const int32_t z = L.sx[i + 1] - L.sx[i];
+                            const int64_t rb = L.sb[i];
+                            for (int32_t e = lane; e < z; e += 64) dw_addk(a.col[rb + e], a.val[rb + e] * cv);
+                        }
+                    }
+                    if (!COCOA_EARLY_RELEASE || pos < 0) {  // (the direct path read the layout and coefficients until here)
+                        wave_lds_sync();
+                        if (lane == 0) {
+                            lds_release(&S.cnt[kCScat + c], b + 1);
+                            if (!COCOA_EARLY_RELEASE && pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                        }
+                    }
+                }
+                // 1. products of the gathers in flight -> this class's part of the base of
+                //    batch xin.  Each unit's product goes to (its row, lane mod 32) with a
+                //    fire-and-forget LDS add (lanes l and l + 32 share a slot: different
+                //    LDS lane groups, no conflict); 4 lanes per row add the slots up.
+                if (xin >= 0) {
+                    if (lane < kGPart) {
+    #pragma unroll
+                        for (int i = 0; i < kGB; ++i) part[i][lane] = 0.0;
                     }
                     wave_lds_sync();
-                    if (lane == 0) lds_release(&S.cnt[kCBase + bslot], x + 1);
-                    publish(x);
+    #pragma unroll
+                    for (int u = 0; u < kGMaxU; ++u) {
+                        if (u < xnu) {
+                            const int row = min((int)((hrow[u / 6] >> (5 * (u % 6))) & 31u), kGB);  // 31: no entry
+                            __hip_atomic_fetch_add(&part[row][lane & (kGPart - 1)], hv[u] * dw[u], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                    wave_lds_sync();
+                    const int rr = lane >> 2, qq = (lane & 3) * (kGPart / 4);
+                    double s4 = 0.0;
+    #pragma unroll
+                    for (int t = 0; t < kGPart / 4; ++t) s4 += part[rr][qq + t];
+                    s4 += dpp_row_d<0xB1>(s4);  // quad_perm [1,0,3,2]
+                    s4 += dpp_row_d<0x4E>(s4);  // quad_perm [2,3,0,1]
+                    if ((lane & 3) == 0) S.base[bslot][(xin % kGNB) * kGB + rr] = s4;
+                    wave_lds_sync();
+                    if (lane == 0) lds_release(&S.cnt[kCBase + bslot], xin + 1);
+                    publish(xin);
+                    xin = -1;
                 }
+                stamp(1);
+                // 3. gathers of batch x = b + kGNB on this class's columns: they see batch
+                //    b's updates (issued above, same wave, same addresses) and nothing later
+                //    (the next atomics go out after step 1 has consumed these loads)
+                const int32_t x = b + kGNB;
+                if (bases && x < NB) {
+                    const GLay& L = S.lay[x % kGRing][c];
+                    const int32_t pos = L.pos, nu = L.nu;
+                    if (pos >= 0) {
+                        if (!fetched(x)) break;
+    #pragma unroll
+                        for (int w = 0; w < (kGMaxU + 5) / 6; ++w) hrow[w] = 0xFFFFFFFFu;  // units past nu: never read
+                        // groups of 4 units (a group past the batch is skipped whole)
+    #pragma unroll
+                        for (int u0 = 0; u0 < kGMaxU; u0 += 4) {
+                            if (u0 < nu) {
+                                int rw[4];
+                                int32_t cl[4];
+                                double vl[4];
+    #pragma unroll
+                                for (int t = 0; t < 4; ++t) {
+                                    uint32_t r8;
+                                    ring_get(S, ring_unit(c, pos, u0 + t), lane, cl[t], vl[t], r8);
+                                    rw[t] = r8 | gram_pad(u0 + t, nu);
+                                }
+                                double hx[4];
+    #pragma unroll
+                                for (int t = 0; t < 4; ++t) {
+                                    const int u = u0 + t;
+                                    const int32_t cc = rw[t] < kGB ? cl[t] : -1;
+                                    // a hot (LDS) or empty lane loads the constant 1 -- one register
+                                    // never mixes a global load with an LDS read (that would serialise)
+                                    if (KIND == 1) {  // hot-only wave: LDS
+                                        dw[u] = 1.0;
+                                        hx[t] = hotl[cc >= 0 ? cc : 0];
+                                    } else if (KIND == 2) {  // cold-only wave: the slice
+                                        if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(dwk + (cc >= 0 ? cc : 0));
+                                    } else if (HOTLDS) {
+                                        if (!(COCOA_DIAG_ON && (a.diag & 2))) dw[u] = dw_load(cc >= hot ? dwk + cc : &g_gram_one);
+                                        hx[t] = hotl[(cc >= 0 && cc < hot) ? cc : 0];
+                                    } else if (!(COCOA_DIAG_ON && (a.diag & 2))) {
+                                        // a lane past the batch loads column 0: its product goes to the sink row
+                                        dw[u] = dw_load(dwk + (cc >= 0 ? cc : 0));
+                                    }
+                                }
+                                __builtin_amdgcn_sched_barrier(0);  // all reads of the group out before the products
+    #pragma unroll
+                                for (int t = 0; t < 4; ++t) {
+                                    const int u = u0 + t;
+                                    const bool ok = rw[t] < kGB;
+                                    if (KIND == 1)
+                                        hv[u] = ok ? vl[t] * hx[t] : 0.0;
+                                    else if (KIND == 2)
+                                        hv[u] = vl[t];
+                                    else if (HOTLDS)
+                                        hv[u] = ok ? ((cl[t] < hot) ? vl[t] * hx[t] : vl[t]) : 0.0;
+                                    else
+                                        hv[u] = vl[t];  // past the batch: any value, summed into the sink row
+                                    hrow[u / 6] = (hrow[u / 6] & ~(31u << (5 * (u % 6)))) | ((uint32_t)(ok ? rw[t] : 31) << (5 * (u % 6)));
+                                }
+                            }
+                        }
+                        xin = x;
+                        xnu = nu;
+                    } else {
+                        // too long to stage: gathered and summed here
+                        double* bs = S.base[bslot] + (x % kGNB) * kGB;
+                        for (int i = 0; i < kGB; ++i) {
+                            const int32_t z = L.sx[i + 1] - L.sx[i];
+                            const int64_t rb = L.sb[i];
+                            double acc = 0.0;
+                            for (int32_t e = lane; e < z; e += 64) acc = fma(a.val[rb + e], dw_getk(a.col[rb + e]), acc);
+                            const double t = wave_sum(acc);
+                            if (lane == 0) bs[i] = t;
+                        }
+                        wave_lds_sync();
+                        if (lane == 0) lds_release(&S.cnt[kCBase + bslot], x + 1);
+                        publish(x);
+                    }
+                }
+                stamp(2);
             }
-            stamp(2);
-        }
+        };
+        // (hot_split < hot: the cold class still holds LDS-resident columns: mixed)
+        const bool spec = MIRROR && COCOA_HOTRUNS && HOTLDS && a.hot_split > 0 && a.hot_split <= hot;
+        if (spec && c == 0)
+            mem_loop(std::integral_constant<int, 1>{});
+        else if (spec && a.hot_split == hot)
+            mem_loop(std::integral_constant<int, 2>{});
+        else
+            mem_loop(std::integral_constant<int, 0>{});
         vm_drain();  // the last atomics land before the kernel ends
         if (a.prof && lane == 0)
             for (int i = 0; i < 4; ++i) a.prof[(size_t)k * kProfStride + 48 + 4 * c + i] = ph[i];
@@ -1493,7 +1525,8 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         // x >= kGNB, from its tagged granules into this half's LDS
         if (MODE != MODE_MBCD) {
             const int hp = 1 - h;
-            const int run = 2 * (lane >> 5) + hp;  // lanes 0-31: run hp, 32-63: run 2 + hp
+            const int run0 = gram_mirror_run(0, hp), run1 = gram_mirror_run(1, hp);
+            const int run = (lane >> 5) ? run1 : run0;  // lanes 0-31: the other half's class 0, 32-63: class 1
             const int row = (lane >> 1) & (kGB - 1), half = lane & 1;
             const uint32_t thi = (uint32_t)(a.xtag_epoch & 0xFFF) << 20;
             for (int32_t x = kGNB; x < NB; ++x) {
@@ -1525,8 +1558,8 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 if (half == 0) S.base[run][(x % kGNB) * kGB + row] = __hiloint2double((int)other, (int)mine);
                 wave_lds_sync();
                 if (lane == 0) {
-                    lds_release(&S.cnt[kCBase + hp], x + 1);
-                    lds_release(&S.cnt[kCBase + 2 + hp], x + 1);
+                    lds_release(&S.cnt[kCBase + run0], x + 1);
+                    lds_release(&S.cnt[kCBase + run1], x + 1);
                 }
             }
         }
@@ -1555,7 +1588,9 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
 #pragma unroll
                 for (int c = 0; c < NRUN; ++c)
                     if (!wait_ge(&S.cnt[kCBase + c], g + 1, abortf, a.status,
-                                 !pw ? nullptr : (MIRROR && (c & 1) != h) ? &wait_base_remote : &wait_base_local))
+                                 !pw ? nullptr
+                                     : (MIRROR && c != gram_mirror_run(0, h) && c != gram_mirror_run(1, h)) ? &wait_base_remote
+                                                                                                               : &wait_base_local))
                         return false;
                 if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw)) return false;
             } else if (!wait_ge(&S.cnt[kCLoad], min(g + kGNB + 1, NB), abortf, a.status, pw)) {

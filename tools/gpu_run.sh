@@ -53,7 +53,20 @@ for step in "$@"; do
       line c5_mbsgd --method mbsgd --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
       line c5_localsgd --method localsgd --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
       line c3 --config c3 --steps 10 --warmup 2 --cpu-seconds 8 || exit $?
-      line c4 --config c4 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+      line c4 --config c4 --steps 10 --warmup 2 --gap-max-rounds 1500 --cpu-seconds 20 || exit $? ;;
+    linec4)  # the C4 line alone (gap run to 1e-4, bounded CPU baseline)
+      line c4 --config c4 --steps 10 --warmup 2 --gap-max-rounds 1500 --cpu-seconds 20 || exit $? ;;
+    c4pmc)  # HBM bytes and L2 hits of the C4 kernels (one counter group per pass)
+      C4SHORT="python3 bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline --no-gap"
+      for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TA_BUSY_avr TA_BUSY_max"; do
+        n=$(echo $grp | cut -d' ' -f1)
+        timeout -s KILL 300 rocprofv3 --pmc $grp -d $O/c4pmc_${n}_$TAG -o run --output-format csv -- $C4SHORT \
+          > $O/c4pmc_${n}_$TAG.log 2>&1 || exit $?
+      done
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 60 rocprofv3 --pmc $c -d $O/calib_${c}_$TAG -o run --output-format csv -- tools/ubench/calib \
+          > $O/calib_${c}_$TAG.log 2>&1 || exit $?
+      done ;;
     lineprof)  # rocprofv3 kernel stats of the C3 / C4 / C5 lines (short runs)
       for cfg in ${LINEPROF:-c4 c3 c5_cocoa}; do
         case $cfg in
