@@ -192,6 +192,24 @@ struct cocoa_ctx {
     // items (block, partition range) and the device-order accumulator
     DevBuf fcol16, fbnd, fitems, ftmp;
     int32_t n_fitems = 0, n_fblk = 0;
+    // Private columns (fast CoCoA+ on the chain solver, compact slices): a column
+    // held by ONE entry of a partition never needs a deltaW slot.  Its deltaW is
+    // x_rc * y_r (alpha_r - alpha_r^0) / (lambda n) (CoCoA.scala:181, summed over
+    // the row's visits), so the row's dot with the private part is
+    // y_r qp_r (alpha_r - alpha_r^0) / (lambda n), qp_r = the private entries'
+    // sum of squares, and the fold adds the private entries' deltaW (formed by
+    // the solver's epilogue).  Slices then hold the shared columns only (max_uh
+    // positions; C4: ~15 k of ~60 k), each row stores its shared entries first
+    // (pcol_h / pval_h, row_zs shared entries), and the private entries form a
+    // per-partition tail sorted by device column (trow / tval: their deltaW is
+    // tval * rowcoef[trow], rowcoef written by the solver's epilogue) beside the
+    // head's fold structures (fbnd_h / fcol16_h / fitems_h; tbnd / tcol16 for
+    // the tail).
+    bool priv_ready = false, dw_priv = false;
+    int64_t max_uh = 0, sum_uh = 0, n_tail = 0;
+    DevBuf pcol_h, pval_h, row_zs, row_qp, rowcoef;
+    DevBuf fcol16_h, fbnd_h, fitems_h, tbnd, tcol16, trow, tval;
+    int32_t n_fitems_h = 0;
     int32_t max_nl = 0, min_nl = 0;
     // test data (this rank)
     Csr te;
@@ -633,11 +651,153 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
 static void set_test_impl(cocoa_ctx* ctx, bool dense_in, const int64_t* row_ptr, const int32_t* col,
                           const double* val, const double* y, int64_t n_rows);
 
+// Work items of the column-block fold: block b's partition range cut into
+// pieces of about kFoldItem entries (cnt(b, k): the entries of partition k in
+// block b); (block, k0, k1, sole), sole = the block's only item (plain stores).
+template <class F>
+static std::vector<int32_t> fold_items(int64_t nblk, int K, F cnt) {
+    std::vector<int32_t> items;
+    for (int64_t b = 0; b < nblk; ++b) {
+        int64_t acc = 0;
+        int k0 = 0;
+        const size_t first = items.size();
+        for (int k = 0; k < K; ++k) {
+            acc += cnt(b, k);
+            if (acc >= kFoldItem || k == K - 1) {
+                items.insert(items.end(), {(int32_t)b, k0, k + 1, 0});
+                k0 = k + 1;
+                acc = 0;
+            }
+        }
+        if (items.size() - first == 4) items[first + 3] = 1;
+    }
+    return items;
+}
+
+// Private-column layout (cocoa_ctx::priv_ready; fast mode, COCOA_DW_PRIVATE=0
+// turns it off).  lists[k]: partition k's distinct device columns in device
+// order; pcol / val: the rows as the fast kernels store them.
+static void build_private(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* pcol, const double* val,
+                          const std::vector<std::vector<int32_t>>& lists) {
+    c->priv_ready = false;
+    for (DevBuf* b : {&c->pcol_h, &c->pval_h, &c->row_zs, &c->row_qp, &c->fcol16_h, &c->fbnd_h, &c->fitems_h, &c->tbnd,
+                      &c->tcol16, &c->trow, &c->tval})
+        b->free();
+    c->n_fitems_h = 0;
+    c->max_uh = c->sum_uh = c->n_tail = 0;
+    const char* env = std::getenv("COCOA_DW_PRIVATE");
+    if (c->strict || (env && !std::atoi(env))) return;
+    const int K = c->K_loc;
+    const int64_t d = c->d, nnz = c->tr.nnz, n = c->tr.n;
+    if (n >= ((int64_t)1 << 31)) return;
+    const int64_t J = kFoldJ, nblk = (d + J - 1) / J;
+    std::vector<int32_t> ncol((size_t)std::max<int64_t>(nnz, 1));
+    std::vector<double> nval((size_t)std::max<int64_t>(nnz, 1));
+    std::vector<int32_t> zs((size_t)std::max<int64_t>(n, 1));
+    std::vector<double> qp((size_t)std::max<int64_t>(n, 1));
+    std::vector<std::vector<int32_t>> heads((size_t)K);
+    struct TailE {
+        int32_t j, r;
+        double v;
+    };
+    std::vector<std::vector<TailE>> tails((size_t)K);
+    const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int tix = 0; tix < T; ++tix)
+        th.emplace_back([&, tix] {
+            std::vector<int32_t> cnt((size_t)d, 0), idx((size_t)d, 0);
+            for (int k = tix; k < K; k += T) {
+                const int64_t r0 = c->h_part_ptr[(size_t)k], r1 = c->h_part_ptr[(size_t)k + 1];
+                for (int64_t q = row_ptr[r0]; q < row_ptr[r1]; ++q) cnt[(size_t)pcol[q]]++;
+                std::vector<int32_t>& Hd = heads[(size_t)k];
+                for (int32_t j : lists[(size_t)k])
+                    if (cnt[(size_t)j] >= 2) idx[(size_t)j] = (int32_t)Hd.size(), Hd.push_back(j);
+                std::vector<TailE>& Tl = tails[(size_t)k];
+                for (int64_t r = r0; r < r1; ++r) {
+                    const int64_t b = row_ptr[r], e = row_ptr[r + 1];
+                    int64_t zsh = 0;
+                    for (int64_t q = b; q < e; ++q) zsh += cnt[(size_t)pcol[q]] >= 2;
+                    int64_t ds = b, dp = b + zsh;
+                    double s2 = 0.0;
+                    for (int64_t q = b; q < e; ++q) {  // shared entries first, each part in stored order
+                        const int32_t j = pcol[q];
+                        if (cnt[(size_t)j] >= 2) {
+                            ncol[(size_t)ds] = idx[(size_t)j];
+                            nval[(size_t)ds++] = val[q];
+                        } else {
+                            ncol[(size_t)dp] = 0;  // (never read: the solver stops at row_zs)
+                            nval[(size_t)dp++] = val[q];
+                            s2 += val[q] * val[q];
+                            Tl.push_back({j, (int32_t)r, val[q]});
+                        }
+                    }
+                    zs[(size_t)r] = (int32_t)zsh;
+                    qp[(size_t)r] = s2;
+                }
+                std::sort(Tl.begin(), Tl.end(), [](const TailE& x, const TailE& y) { return x.j < y.j; });
+                for (int32_t j : lists[(size_t)k]) cnt[(size_t)j] = 0;
+            }
+        });
+    for (auto& t : th) t.join();
+    int64_t mu = 1, su = 0, nt = 0;
+    for (auto& Hd : heads) mu = std::max<int64_t>(mu, (int64_t)Hd.size()), su += (int64_t)Hd.size();
+    for (auto& Tl : tails) nt += (int64_t)Tl.size();
+    if ((uint64_t)K * (uint64_t)mu >= ((uint64_t)1 << 32) || nt >= ((int64_t)1 << 31)) return;
+    // the head's fold structures, as build_compact's over the shared columns
+    std::vector<uint32_t> bnd((size_t)(nblk + 1) * (size_t)K), tb((size_t)(nblk + 1) * (size_t)K);
+    std::vector<uint16_t> fc((size_t)K * (size_t)mu, 0);
+    std::vector<int32_t> trw((size_t)std::max<int64_t>(nt, 1));
+    std::vector<uint16_t> tc((size_t)std::max<int64_t>(nt, 1));
+    std::vector<double> tv((size_t)std::max<int64_t>(nt, 1));
+    int64_t toff = 0;
+    for (int k = 0; k < K; ++k) {
+        const std::vector<int32_t>& L = heads[(size_t)k];
+        const std::vector<TailE>& Tl = tails[(size_t)k];
+        size_t i = 0, t = 0;
+        for (int64_t b = 0; b <= nblk; ++b) {
+            while (i < L.size() && L[i] < b * J) ++i;
+            while (t < Tl.size() && Tl[t].j < b * J) ++t;
+            bnd[(size_t)b * K + k] = (uint32_t)i;
+            tb[(size_t)b * K + k] = (uint32_t)(toff + (int64_t)t);
+        }
+        for (size_t q = 0; q < L.size(); ++q) fc[(size_t)k * mu + q] = (uint16_t)(L[q] & (J - 1));
+        for (size_t q = 0; q < Tl.size(); ++q) {
+            trw[(size_t)toff + q] = Tl[q].r;
+            tc[(size_t)toff + q] = (uint16_t)(Tl[q].j & (J - 1));
+            tv[(size_t)toff + q] = Tl[q].v;
+        }
+        toff += (int64_t)Tl.size();
+    }
+    const std::vector<int32_t> items = fold_items(nblk, K, [&](int64_t b, int k) -> int64_t {
+        return (int64_t)(bnd[(size_t)(b + 1) * K + k] - bnd[(size_t)b * K + k]) +
+               (int64_t)(tb[(size_t)(b + 1) * K + k] - tb[(size_t)b * K + k]);
+    });
+    hipStream_t s = c->stream;
+    upload_padded(c->pcol_h, ncol.data(), sizeof(int32_t) * (size_t)nnz, s);
+    upload_padded(c->pval_h, nval.data(), sizeof(double) * (size_t)nnz, s);
+    upload(c->row_zs, zs.data(), sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1), s);
+    upload(c->row_qp, qp.data(), sizeof(double) * (size_t)std::max<int64_t>(n, 1), s);
+    upload(c->fbnd_h, bnd.data(), sizeof(uint32_t) * bnd.size(), s);
+    upload_padded(c->fcol16_h, fc.data(), sizeof(uint16_t) * fc.size(), s);
+    upload(c->fitems_h, items.data(), sizeof(int32_t) * items.size(), s);
+    upload(c->tbnd, tb.data(), sizeof(uint32_t) * tb.size(), s);
+    upload_padded(c->trow, trw.data(), sizeof(int32_t) * trw.size(), s);
+    upload_padded(c->tcol16, tc.data(), sizeof(uint16_t) * tc.size(), s);
+    upload_padded(c->tval, tv.data(), sizeof(double) * tv.size(), s);
+    HIPCHK(hipStreamSynchronize(s));
+    c->n_fitems_h = (int32_t)(items.size() / 4);
+    c->max_uh = mu;
+    c->sum_uh = su;
+    c->n_tail = nt;
+    c->priv_ready = true;
+}
+
 // Compact deltaW layout (see cocoa_ctx::compact_ready).  COCOA_DW_COMPACT=0 / 1
 // forces it off / on (tests); on by default once K_loc * d * 8 >= 1 GiB and the
 // distinct columns per partition are fewer than d / 4.
-static void build_compact(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* pcol) {
+static void build_compact(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* pcol, const double* val) {
     c->compact_ready = false;
+    c->priv_ready = false;
     c->col_local.free();
     c->fptr.free();
     c->fpos.free();
@@ -707,21 +867,9 @@ static void build_compact(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* p
             }
             for (size_t q = 0; q < L.size(); ++q) fc[(size_t)k * mu + q] = (uint16_t)(L[q] & (J - 1));
         }
-        std::vector<int32_t> items;  // (block, k0, k1, sole)
-        for (int64_t b = 0; b < nblk; ++b) {
-            int64_t acc = 0;
-            int k0 = 0;
-            const size_t first = items.size();
-            for (int k = 0; k < K; ++k) {
-                acc += bnd[(size_t)(b + 1) * K + k] - bnd[(size_t)b * K + k];
-                if (acc >= kFoldItem || k == K - 1) {
-                    items.insert(items.end(), {(int32_t)b, k0, k + 1, 0});
-                    k0 = k + 1;
-                    acc = 0;
-                }
-            }
-            if (items.size() - first == 4) items[first + 3] = 1;  // the block's only item: plain stores
-        }
+        const std::vector<int32_t> items = fold_items(nblk, K, [&](int64_t b, int k) -> int64_t {
+            return (int64_t)(bnd[(size_t)(b + 1) * K + k] - bnd[(size_t)b * K + k]);
+        });
         upload(c->fbnd, bnd.data(), sizeof(uint32_t) * bnd.size(), s);
         upload_padded(c->fcol16, fc.data(), sizeof(uint16_t) * fc.size(), s);
         upload(c->fitems, items.data(), sizeof(int32_t) * items.size(), s);
@@ -733,6 +881,7 @@ static void build_compact(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* p
     c->max_u = mu;
     c->sum_u = su;
     c->compact_ready = true;
+    build_private(c, row_ptr, pcol, val, lists);
 }
 
 // ------------------------------------------------------------------- data --
@@ -951,14 +1100,15 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     upload(ctx->sqn, sq.data(), sizeof(double) * (size_t)n_rows, s);
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
-    ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s, eval_tile_entries());
+    ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s, eval_tile_entries(num_features));
     if (dense_in) {
         ctx->compact_ready = false;  // dense rows touch every column: no compact slices
+        ctx->priv_ready = false;
         ctx->col_local.free();
         ctx->fptr.free();
         ctx->fpos.free();
     } else {
-        build_compact(ctx, row_ptr, pcol.data());
+        build_compact(ctx, row_ptr, pcol.data(), split_classes ? pval.data() : val);
     }
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = false;
@@ -1006,7 +1156,7 @@ static void set_test_impl(cocoa_ctx* ctx, bool dense_in, const int64_t* row_ptr,
     }
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
-    ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s, eval_tile_entries());
+    ctx->n_t_tiles = make_tiles(row_ptr, n_rows, ctx->t_tiles, s, eval_tile_entries(ctx->d));
     HIPCHK(hipStreamSynchronize(s));
     ctx->has_test = true;
     ctx->n_test_glob = -1;  // (re-exchanged at the next multi-rank cocoa_eval_begin)
@@ -1090,7 +1240,7 @@ static void plan_solver(cocoa_ctx* c, int64_t vec_len, bool need_prod = true) {
         !(he && !std::atoi(he))) {
         const size_t lim = want > 1 ? budget : kLdsMax;
         const int64_t h = off < lim ? std::min<int64_t>((int64_t)((lim - off) / sizeof(double)) & ~(int64_t)63,
-                                                        c->max_u)
+                                                        vec_len)
                                     : 0;
         if (h >= 64) {
             a.hot = (int32_t)h;
@@ -1180,21 +1330,62 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     // column, so CoCoA keeps the dense slices.
     ctx->dw_compact = ctx->compact_ready && (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_MBCD) &&
                       params->local_iters >= 1 && !(ctx->tr_dense && dense_solver_fits(d, ctx->max_nl));
-    const int64_t slice = ctx->dw_compact ? ctx->max_u : d;
+    // the loader of the SDCA solvers (and of local SGD on the Gram solver) is
+    // fed by the per-step plan; set below, once the solver is chosen
+    // fast SDCA: the Gram-window solver, unless the rows are dense-long (C3:
+    // 2,000 entries per row, where the chain solver streams w / deltaW from LDS)
+    const double zavg = ctx->tr.n ? (double)ctx->tr.nnz / (double)ctx->tr.n : 0.0;
+    ctx->use_dense = !ctx->strict && is_sdca(method) && H >= 1 && ctx->tr_dense &&
+                     dense_solver_fits(d, ctx->max_nl) &&
+                     (ctx->solver_kind == COCOA_SOLVER_DENSE || ctx->solver_kind == COCOA_SOLVER_AUTO);
+    require(ctx->use_dense || ctx->solver_kind != COCOA_SOLVER_DENSE || ctx->strict || !is_sdca(method), COCOA_E_ARG,
+            "cocoa_init: the dense solver needs dense rows (cocoa_set_train_dense) with an even d <= 4096 and "
+            "partitions of at most 19,200 rows");
+    // AUTO takes the Gram solver when its side work has idle CUs to run on: at
+    // most one partition per CU (C2: 64 on 256 CUs).  With more partitions than
+    // CUs (C4 on one GPU: 1,024) every CU already runs chains and the Gram rows
+    // (measured: 46 ms per C4 round on the side stream) only compete with them.
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    ctx->ncu = ncu;
+    // local SGD runs on the Gram solver too (MODE_LSGD, dense slices: its
+    // epilogue reads wInit by the slice's column)
+    const bool gram_method = is_sdca(method) || (method == COCOA_METHOD_LOCALSGD && !ctx->dw_compact);
+    ctx->use_gram = !ctx->strict && !ctx->use_dense && gram_method && H >= 1 &&
+                    (ctx->solver_kind == COCOA_SOLVER_GRAM ||
+                     (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0 && K <= ncu));
+    // private columns (cocoa_ctx::priv_ready): fast CoCoA+ on the chain solver
+    // over compact slices, folded by column blocks (so double-buffered)
+    ctx->dw_priv = ctx->dw_compact && ctx->priv_ready && !ctx->strict && method == COCOA_METHOD_COCOA_PLUS &&
+                   !ctx->use_gram && !ctx->use_dense && ctx->n_fitems_h > 0;
+    int64_t slice = 0;
+    for (;;) {
+        slice = ctx->dw_priv ? ctx->max_uh : ctx->dw_compact ? ctx->max_u : d;
+        // a second deltaW set only when it fits next to everything else (with 1 GiB
+        // to spare); otherwise single buffering with the zero-in-fold path.  Compact
+        // slices (C4: 1,024 x 64,847 doubles, 0.53 GB a set) take the second set
+        // too: the fold then only reads, and the set it folded is re-zeroed by a
+        // streaming memset beside the next round's solver instead of by 62 M
+        // scattered 8-byte stores.
+        ctx->dw_dbuf = dw_double_buffer((size_t)(K * slice) * sizeof(double), ctx->dw_compact);
+        if (ctx->dw_dbuf) {
+            ctx->dw2.free();
+            size_t free_b = 0, total_b = 0;
+            HIPCHK(hipMemGetInfo(&free_b, &total_b));
+            if (free_b < 2 * sizeof(double) * (size_t)(K * slice) + ((size_t)1 << 30)) ctx->dw_dbuf = false;
+        }
+        if (ctx->dw_priv && !ctx->dw_dbuf) {  // (the gather fold has no private tail)
+            ctx->dw_priv = false;
+            continue;
+        }
+        break;
+    }
     ctx->dw_slice = slice;
     ctx->dw.alloc_zero(sizeof(double) * (size_t)(K * slice), s);
-    // a second deltaW set only when it fits next to everything else (with 1 GiB
-    // to spare); otherwise single buffering with the zero-in-fold path.  Compact
-    // slices (C4: 1,024 x 64,847 doubles, 0.53 GB a set) take the second set
-    // too: the fold then only reads, and the set it folded is re-zeroed by a
-    // streaming memset beside the next round's solver instead of by 62 M
-    // scattered 8-byte stores.
-    ctx->dw_dbuf = dw_double_buffer((size_t)(K * slice) * sizeof(double), ctx->dw_compact);
-    if (ctx->dw_dbuf) {
-        size_t free_b = 0, total_b = 0;
-        HIPCHK(hipMemGetInfo(&free_b, &total_b));
-        if (free_b < sizeof(double) * (size_t)(K * slice) + ((size_t)1 << 30)) ctx->dw_dbuf = false;
-    }
+    if (ctx->dw_priv)
+        ctx->rowcoef.alloc(sizeof(double) * (size_t)std::max<int64_t>(n, 1));
+    else
+        ctx->rowcoef.free();
     if (ctx->dw_dbuf) {
         ctx->dw2.alloc_zero(sizeof(double) * (size_t)(K * slice), s);
         if (!ctx->zstream) {
@@ -1228,8 +1419,11 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.row_ptr = ctx->tr.row_ptr.as<int64_t>();
     // compact slices: the solvers index deltaW by the entry's slice position
     // (x.w comes from the plan, which reads the global columns)
-    a.col = ctx->dw_compact ? ctx->col_local.as<int32_t>() : ctx->tr.col.as<int32_t>();
-    a.val = ctx->tr.val.as<double>();
+    a.col = ctx->dw_priv ? ctx->pcol_h.as<int32_t>() : ctx->dw_compact ? ctx->col_local.as<int32_t>()
+                                                                        : ctx->tr.col.as<int32_t>();
+    a.val = ctx->dw_priv ? ctx->pval_h.as<double>() : ctx->tr.val.as<double>();
+    a.row_qp = ctx->dw_priv ? ctx->row_qp.as<double>() : nullptr;
+    a.rowcoef = ctx->dw_priv ? ctx->rowcoef.as<double>() : nullptr;
     a.y = ctx->tr.y.as<double>();
     a.sqn = ctx->sqn.as<double>();
     a.rowflags = ctx->rowflags.as<uint8_t>();
@@ -1250,36 +1444,13 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     a.sigma = Kg * params->gamma;                                            // CoCoA.scala:45
     a.scaling = ctx->scaling;
 
-    // the loader of the SDCA solvers (and of local SGD on the Gram solver) is
-    // fed by the per-step plan; set below, once the solver is chosen
-    // fast SDCA: the Gram-window solver, unless the rows are dense-long (C3:
-    // 2,000 entries per row, where the chain solver streams w / deltaW from LDS)
-    const double zavg = ctx->tr.n ? (double)ctx->tr.nnz / (double)ctx->tr.n : 0.0;
-    ctx->use_dense = !ctx->strict && is_sdca(method) && H >= 1 && ctx->tr_dense &&
-                     dense_solver_fits(d, ctx->max_nl) &&
-                     (ctx->solver_kind == COCOA_SOLVER_DENSE || ctx->solver_kind == COCOA_SOLVER_AUTO);
-    require(ctx->use_dense || ctx->solver_kind != COCOA_SOLVER_DENSE || ctx->strict || !is_sdca(method), COCOA_E_ARG,
-            "cocoa_init: the dense solver needs dense rows (cocoa_set_train_dense) with an even d <= 4096 and "
-            "partitions of at most 19,200 rows");
-    // AUTO takes the Gram solver when its side work has idle CUs to run on: at
-    // most one partition per CU (C2: 64 on 256 CUs).  With more partitions than
-    // CUs (C4 on one GPU: 1,024) every CU already runs chains and the Gram rows
-    // (measured: 46 ms per C4 round on the side stream) only compete with them.
-    int ncu = 256;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    ctx->ncu = ncu;
     // every local solver but the dense one reads the column array (and the
     // dense rows of cocoa_set_train_dense have none yet)
     if (ctx->strict || !ctx->use_dense) {
         ensure_cols(ctx->tr, ctx->d, s);
-        a.col = ctx->dw_compact ? ctx->col_local.as<int32_t>() : ctx->tr.col.as<int32_t>();
+        a.col = ctx->dw_priv ? ctx->pcol_h.as<int32_t>() : ctx->dw_compact ? ctx->col_local.as<int32_t>()
+                                                                            : ctx->tr.col.as<int32_t>();
     }
-    // local SGD runs on the Gram solver too (MODE_LSGD, dense slices: its
-    // epilogue reads wInit by the slice's column)
-    const bool gram_method = is_sdca(method) || (method == COCOA_METHOD_LOCALSGD && !ctx->dw_compact);
-    ctx->use_gram = !ctx->strict && !ctx->use_dense && gram_method && H >= 1 &&
-                    (ctx->solver_kind == COCOA_SOLVER_GRAM ||
-                     (ctx->solver_kind == COCOA_SOLVER_AUTO && zavg <= 512.0 && K <= ncu));
     ctx->use_plan = is_sdca(method) || ctx->use_gram;
     ctx->gram_mirror = false;
     if (ctx->use_gram) {
@@ -1303,9 +1474,14 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                 // the mirrored solver (CoCoA+ / CoCoA, 4 K <= CUs; COCOA_GRAM_MIRROR=0 turns it
                 // off): two workgroups per partition, the Gram rows on the rest.  C2 (r06l,
                 // one box): solver 2.62 -> 2.39 ms, step 2.92 -> 2.70
+                // Only past the window's batches: the halves first trade bases at batch
+                // kGNB, and a half finishing before the other starts would overwrite the
+                // alphaOld that half still copies in (found as an intermittent wrong w at
+                // H = 10 with four members sharing one GPU)
                 const char* me = std::getenv("COCOA_GRAM_MIRROR");
                 ctx->gram_mirror = !(me && !std::atoi(me)) && 4 * kk <= ncu && !ctx->dw_compact && ctx->row_zc.p &&
-                                   (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_COCOA);
+                                   (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_COCOA) &&
+                                   ctx->nbatch > gram_window_batches();
                 if (ctx->gram_mirror) ctx->xbase.alloc_zero(sizeof(uint64_t) * (size_t)kk * kGramRuns * kXbR * 32, s);
                 else ctx->xbase.free();
                 const int used = (ctx->gram_mirror ? 2 : 1) * kk;
@@ -1447,6 +1623,7 @@ static PlanArgs plan_args(cocoa_ctx* c, const int32_t* samples, int set) {
     pa.steps = (int64_t)c->K_loc * c->P.local_iters;
     pa.H = c->P.local_iters;
     pa.row_zc = c->plan_zc.p ? c->row_zc.as<int32_t>() : nullptr;
+    pa.row_zs = c->dw_priv ? c->row_zs.as<int32_t>() : nullptr;  // (the chain's rows: shared entries only)
     pa.zc = !c->plan_zc.p ? nullptr : set ? c->plan_zc2.as<int32_t>() : c->plan_zc.as<int32_t>();
     pa.beg = set ? c->plan_beg2.as<int64_t>() : c->plan_beg.as<int64_t>();
     pa.z = set ? c->plan_z2.as<int32_t>() : c->plan_z.as<int32_t>();
@@ -1755,7 +1932,14 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
     }
     if (produce) HIPCHK(hipStreamWaitEvent(s, c->e_xw, 0));  // its reads of w are done
     c->timed(COCOA_K_FOLD, [&] {
-        if (c->dw_compact && c->n_fitems > 0 && c->dw_dbuf && !chain_init)
+        if (c->dw_priv) {
+            require(!chain_init, COCOA_E_STATE, "private columns need the column-block fold");
+            FoldTail tl{c->tbnd.as<uint32_t>(), c->tcol16.as<uint16_t>(), c->trow.as<int32_t>(), c->tval.as<double>(),
+                        c->rowcoef.as<double>()};
+            launch_fold_blocks(dws, c->fcol16_h.as<uint16_t>(), c->fbnd_h.as<uint32_t>(), c->fitems_h.as<int32_t>(),
+                               c->n_fitems_h, K, c->max_uh, d, c->ftmp.as<double>(), c->dw_sum, c->w.as<double>(),
+                               c->mult, fuse_apply, c->d_inv.as<int32_t>(), s, &tl);
+        } else if (c->dw_compact && c->n_fitems > 0 && c->dw_dbuf && !chain_init)
             launch_fold_blocks(dws, c->fcol16.as<uint16_t>(), c->fbnd.as<uint32_t>(), c->fitems.as<int32_t>(),
                                c->n_fitems, K, c->max_u, d, c->ftmp.as<double>(), c->dw_sum, c->w.as<double>(),
                                c->mult, fuse_apply, c->d_inv.as<int32_t>(), s);
@@ -2665,6 +2849,8 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     a.plan_beg = nullptr;  // the unit API stages its rows itself
     a.plan_z = nullptr;
     a.plan_y = a.plan_q = a.plan_xw = nullptr;
+    a.row_qp = nullptr;  // (the full rows and a dense deltaW)
+    a.rowcoef = nullptr;
     a.d = d;
     a.H = local_iters;
     a.any_dup = ctx->any_dup ? 1 : 0;
@@ -2692,7 +2878,7 @@ extern "C" int cocoa_local_sdca(cocoa_ctx* ctx, int32_t part, double* w, int32_t
     if (!plus) ctx->to_host_order(wdev, w);
     if (delta_alpha)
         for (int32_t i = 0; i < nl; ++i) delta_alpha[i] = alpha[i] - old[(size_t)i];  // CoCoA.scala:190
-    if (ctx->inited) plan_solver(ctx, ctx->dw_compact ? ctx->max_u : d, !is_sdca(ctx->method));
+    if (ctx->inited) plan_solver(ctx, ctx->dw_slice, !is_sdca(ctx->method));
     CAPI_END(ctx)
 }
 
@@ -3256,7 +3442,8 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "{\"gram_chunks\":%d,\"gram_fallback_last\":%d,\"gram_mirror\":%d,\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
-                  "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d}",
+                  "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d,"
+                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld}",
                   ctx->use_gram ? ctx->gram_chunks : 0, gfb, ctx->gram_mirror ? 1 : 0,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
@@ -3264,6 +3451,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   ctx->dw_dbuf ? 1 : 0, ctx->use_dense ? "dense" : ctx->use_gram ? "gram" : "chain",
                   ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u,
                   !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
-                  ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot);
+                  ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot, ctx->dw_priv ? 1 : 0,
+                  (long long)ctx->max_uh, (long long)ctx->n_tail);
     CAPI_END(ctx)
 }

@@ -61,6 +61,7 @@ struct BatchMeta {
     double q[kMetaSteps];      // Math.pow(norm(x), 2)
     double xw[kMetaSteps];     // x . w (read-only w: CoCoA+ and MbCD), summed in stored order
     double rq[kMetaSteps];     // fast mode: 1 / qii, so the chain multiplies instead of dividing
+    double pq[kMetaSteps];     // private columns: y qp / (lambda n) (xw then holds x.w - sigma pq alpha^0), else 0
     int32_t m;                 // steps in this batch (0 = no more work)
     int32_t pad[3];
 };
@@ -87,6 +88,13 @@ struct SolverArgs {
     const double* plan_y;
     const double* plan_q;
     const double* plan_xw;
+    // private columns (fast CoCoA+, cocoa_ctx::priv_ready): per row the private
+    // entries' sum of squares (the row's dot with them is y qp (alpha - alpha^0) /
+    // (lambda n)); the epilogue stores rowcoef = y (alpha - alpha^0) / (lambda n)
+    // per row (the fold's tail multiplies it by each private entry's value).
+    // Both null otherwise.
+    const double* row_qp;
+    double* rowcoef;
     int64_t d;
     int32_t H;
     int32_t stream_cap;       // staged entries per batch buffer
@@ -126,6 +134,7 @@ struct PlanArgs {
     int32_t need_xw;
     const double* xw_cache;   // per-row x.w of the current w from the last fast eval, or null
     const int32_t* row_zc;    // per row: 4 int32, ends of the class runs 0 .. kGramClasses-2 (fast mode), or null
+    const int32_t* row_zs;    // private columns: per row its shared entries (the step's z), or null
     int64_t* beg;
     int32_t* z;
     int32_t* zc;              // per step: row_zc of its row, 4 int32 (when row_zc)
@@ -296,13 +305,19 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
 // returns true when the sums were also stored to a.out_host (no copy needed)
 bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s);
 int eval_fast_blocks(int64_t n, int64_t n_test);
-int eval_tile_entries();  // entries per fast-eval tile (make_tiles cap)
+// entries per fast-eval tile (make_tiles cap).  Past kEvalWideD columns (w
+// beyond the L2s, int32 columns: C4) the pass takes 2,048-entry tiles and keeps
+// w's 4,096 most frequent columns in LDS, three workgroups per CU (C4, same
+// box: 1.36 -> 1.21 ms; the same on C2's uint16 columns: 0.213 -> 0.220)
+constexpr int64_t kEvalWideD = 65536;
+int eval_tile_entries(int64_t d);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 // Gram-window solver: lds bytes for a partition of max_nl rows (alpha in LDS
 // when it fits, else in alpha_work)
 size_t gram_solver_lds(int64_t d, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
 size_t gram_seq_lds();  // LDS bytes of gram_seq_kernel (one workgroup per CU)
+int gram_window_batches();  // batches in the Gram solver's look-back window (kGNB)
 void launch_xw_produce(const XwArgs& a, hipStream_t s);
 void launch_xw_gather(const int64_t* part_ptr, const int32_t* samples, int32_t H, int64_t steps,
                       const double* row_xw, double* xw, hipStream_t s);
@@ -334,9 +349,20 @@ void launch_fold(const double* dw, int32_t K, int64_t d, double* dw_sum, double*
 // (the double-buffered set is re-zeroed by a memset)
 constexpr int64_t kFoldJ = 4096;
 constexpr int64_t kFoldItem = 32768;
+// the private columns' tail (cocoa_ctx::priv_ready): per (block, partition) the
+// run [tbnd[b K + k], tbnd[(b+1) K + k]) of the flattened tail, each entry its
+// column's offset in the block, its row and value; its deltaW is
+// val * rowcoef[row] (rowcoef: the solver's epilogue)
+struct FoldTail {
+    const uint32_t* tbnd;
+    const uint16_t* tcol16;
+    const int32_t* trow;
+    const double* tval;
+    const double* rowcoef;
+};
 void launch_fold_blocks(const double* dw, const uint16_t* fcol16, const uint32_t* fbnd, const int32_t* items,
                         int32_t n_items, int32_t K, int64_t max_u, int64_t d, double* tmp, double* dw_sum, double* w,
-                        double mult, bool apply, const int32_t* inv, hipStream_t s);
+                        double mult, bool apply, const int32_t* inv, hipStream_t s, const FoldTail* tail = nullptr);
 void launch_fold_compact(double* dw, const int64_t* fptr, const uint32_t* fpos, int64_t d, double* dw_sum, double* w,
                          double mult, bool apply, const int32_t* inv, bool zero, hipStream_t s,
                          const double* init = nullptr);

@@ -65,8 +65,11 @@ size_t gram_seq_lds() { return sizeof(GramSeqLds); }
 // solver workgroup (both grids deal k round robin).  Publication
 // (MI355X_MICROARCH.md, inter-workgroup visibility, the write-through form):
 // sc1 (agent-scope relaxed) stores, every wave's vmcnt(0), a barrier, then one
-// lane's sc1 flag store; the loader polls the flags and loads the values with
-// sc1 loads (solver_gram.h).  No release fence: an L2 write-back per block
+// lane's sc1 flag store; the loader polls the flags, takes one agent acquire per
+// 16 batches (these blocks run several per CU, outside the guide's one-per-CU
+// sc1-load row) and loads the values with sc1 loads (solver_gram.h).  Every
+// value is stored sc1 and drained before its flag, so the flag store needs no
+// release fence either (the guide's sc1 producer form).  An L2 write-back per block
 // (buffer_wbl2) also flushed the solver's freshly dirtied deltaW lines and took
 // the producer to 2.0-2.4 ms and the solver beside it to 4.7 ms (r04m).
 __global__ __launch_bounds__(256) void xw_produce_kernel(XwArgs a) {
@@ -86,6 +89,8 @@ __global__ __launch_bounds__(256) void xw_produce_kernel(XwArgs a) {
     if (tid == 0)
         __hip_atomic_store(a.flag + (size_t)k * a.nbatch + b, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+int gram_window_batches() { return kGNB; }
 
 void launch_xw_produce(const XwArgs& a, hipStream_t s) {
     // 4 KB of (unused) LDS: a block then never fits beside a Gram-solver
@@ -494,9 +499,10 @@ static int eval_variant() {
     }
     return v;
 }
-int eval_tile_entries() {
+int eval_tile_entries(int64_t d) {
     if (const char* e = getenv("COCOA_EVAL_TILE")) return atoi(e) == 2048 ? 2048 : kEvalTile;
-    return (eval_variant() >= 6 && eval_variant() <= 9) ? 2048 : kEvalTile;
+    if (eval_variant() >= 6 && eval_variant() <= 9) return 2048;
+    return d > kEvalWideD ? 2048 : kEvalTile;
 }
 
 static bool launch_eval_diag(const EvalArgs& a, bool c16, hipStream_t s) {
@@ -516,29 +522,41 @@ static bool launch_eval_diag(const EvalArgs& a, bool c16, hipStream_t s) {
         }
         return true;
     }
-    if (v >= 5 && c16) {  // hot w columns in LDS (uint16 columns only)
+    // hot w columns in LDS, and the timing diagnostics, for either column width
+#define COCOA_EVAL_C16(...)                          \
+    do {                                             \
+        if (c16) {                                   \
+            constexpr bool C = true;                 \
+            __VA_ARGS__;                             \
+        } else {                                     \
+            constexpr bool C = false;                \
+            __VA_ARGS__;                             \
+        }                                            \
+    } while (0)
+    if (v >= 5) {
         const int nb = eval_fast_blocks(a.n_tiles, a.n_t_tiles);
         if (v == 5) {  // 4,096-entry tiles, 32 KB of w: 2 blocks per CU
             const int n2 = (int)std::min<int64_t>(a.n_tiles + a.n_t_tiles, 512);
-            eval_stream_kernel<kEvalTile, 512, true, 0, 4096><<<n2, 512, 0, s>>>(a);
+            COCOA_EVAL_C16((eval_stream_kernel<kEvalTile, 512, C, 0, 4096><<<n2, 512, 0, s>>>(a)));
             eval_final_kernel<<<1, 256, 0, s>>>(a.partials, n2, a.out);
         } else if (v == 6) {  // 2,048-entry tiles, 32 KB of w: 3 blocks per CU
-            eval_stream_kernel<2048, 512, true, 0, 4096><<<nb, 512, 0, s>>>(a);
+            COCOA_EVAL_C16((eval_stream_kernel<2048, 512, C, 0, 4096><<<nb, 512, 0, s>>>(a)));
             eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
         } else {  // 2,048-entry tiles, 64 KB of w (8,192 columns): 2 blocks per CU
             const int n2 = (int)std::min<int64_t>(a.n_tiles + a.n_t_tiles, 512);
-            eval_stream_kernel<2048, 512, true, 0, 8192><<<n2, 512, 0, s>>>(a);
+            COCOA_EVAL_C16((eval_stream_kernel<2048, 512, C, 0, 8192><<<n2, 512, 0, s>>>(a)));
             eval_final_kernel<<<1, 256, 0, s>>>(a.partials, n2, a.out);
         }
         return true;
     }
-    if ((v == 3 || v == 4) && c16) {  // timing diagnostics (results invalid)
+    if (v == 3 || v == 4) {  // timing diagnostics (results invalid)
         const int nb = eval_fast_blocks(a.n_tiles, a.n_t_tiles);
-        if (v == 3) eval_stream_kernel<kEvalTile, 512, true, 1><<<nb, 512, 0, s>>>(a);
-        else eval_stream_kernel<kEvalTile, 512, true, 2><<<nb, 512, 0, s>>>(a);
+        if (v == 3) COCOA_EVAL_C16((eval_stream_kernel<kEvalTile, 512, C, 1><<<nb, 512, 0, s>>>(a)));
+        else COCOA_EVAL_C16((eval_stream_kernel<kEvalTile, 512, C, 2><<<nb, 512, 0, s>>>(a)));
         eval_final_kernel<<<1, 256, 0, s>>>(a.partials, nb, a.out);
         return true;
     }
+#undef COCOA_EVAL_C16
     if (v == 1 || v == 2) {  // one 16-lane group per row, 8 / 4 loads per lane in flight
         const int nb = 2048;
         if (v == 1) {
@@ -554,7 +572,7 @@ static bool launch_eval_diag(const EvalArgs& a, bool c16, hipStream_t s) {
     return false;
 }
 #else
-int eval_tile_entries() { return kEvalTile; }
+int eval_tile_entries(int64_t d) { return d > kEvalWideD ? 2048 : kEvalTile; }
 #endif
 
 bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
@@ -566,6 +584,8 @@ bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
 #endif
     if (c16)
         eval_stream_kernel<kEvalTile, 512, true><<<blocks, 512, 0, s>>>(a);
+    else if (a.d > kEvalWideD)
+        eval_stream_kernel<2048, 512, false, 0, 4096><<<blocks, 512, 0, s>>>(a);
     else
         eval_stream_kernel<kEvalTile, 512, false><<<blocks, 512, 0, s>>>(a);
     if (!a.counter) eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
@@ -591,9 +611,17 @@ bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
 // item is the block's only one, else an fp64 atomic add), and fold_finish
 // moves tmp into the rank's sum (original order) or into w, re-zeroing tmp.
 // Sums are reassociated and atomic: fast mode.
+// TAIL: the private columns' tail (FoldTail) after the slices' runs, with the
+// same packing: entry (row, c, v) adds v * rowcoef[row] to column c.  (Measured
+// on C4, same box: 0.57 ms per fold against 0.21 without the tail; a separate
+// pass forming the tail's deltaW first, partition-major so its rowcoef reads
+// stay in one partition's rows, took 0.32 ms and the fold 0.25 after it; the
+// solver's epilogue forming them, 46 k dependent gathers per workgroup behind
+// its chain, +0.9 ms on the solver.)
+template <bool TAIL>
 __global__ __launch_bounds__(256) void fold_blocks_kernel(const double* dw, const uint16_t* fcol16,
                                                           const uint32_t* fbnd, const int32_t* items, int32_t K,
-                                                          int64_t max_u, int64_t d, double* tmp) {
+                                                          int64_t max_u, int64_t d, double* tmp, FoldTail tl) {
     constexpr int kUn = 4;  // 64-entry pieces per wave in flight
     __shared__ double acc[kFoldJ];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -603,41 +631,57 @@ __global__ __launch_bounds__(256) void fold_blocks_kernel(const double* dw, cons
     __syncthreads();
     // the whole block walks the partitions 64 at a time; the 4 waves share each
     // group's packed entries, kUn pieces of 64 per wave in flight
-    for (int32_t kk = k0; kk < k1; kk += 64) {
-        const int32_t k = kk + lane;
-        const bool ok = k < k1;
-        const int32_t lo = ok ? (int32_t)fbnd[(size_t)b * K + k] : 0;
-        const int32_t n = ok ? (int32_t)fbnd[(size_t)(b + 1) * K + k] - lo : 0;
-        const int32_t incl = wave_incl_scan(n);
-        const int32_t T = __shfl(incl, 63, 64);
-        const int32_t excl = incl - n;
-        for (int32_t q0 = 64 * kUn * wv; q0 < T; q0 += 64 * kUn * 4) {
-            size_t pos[kUn];
-            bool val[kUn];
+    for (int part = 0; part < (TAIL ? 2 : 1); ++part) {
+        const uint32_t* bnd = part ? tl.tbnd : fbnd;
+        for (int32_t kk = k0; kk < k1; kk += 64) {
+            const int32_t k = kk + lane;
+            const bool ok = k < k1;
+            const int32_t lo = ok ? (int32_t)bnd[(size_t)b * K + k] : 0;
+            const int32_t n = ok ? (int32_t)bnd[(size_t)(b + 1) * K + k] - lo : 0;
+            const int32_t incl = wave_incl_scan(n);
+            const int32_t T = __shfl(incl, 63, 64);
+            const int32_t excl = incl - n;
+            for (int32_t q0 = 64 * kUn * wv; q0 < T; q0 += 64 * kUn * 4) {
+                size_t pos[kUn];
+                bool val[kUn];
 #pragma unroll
-            for (int u = 0; u < kUn; ++u) {
-                const int32_t q = q0 + 64 * u + lane;
-                // largest lane j with excl_j <= q (every lane active in the shuffles)
-                int j = 0;
+                for (int u = 0; u < kUn; ++u) {
+                    const int32_t q = q0 + 64 * u + lane;
+                    // largest lane j with excl_j <= q (every lane active in the shuffles)
+                    int j = 0;
 #pragma unroll
-                for (int st = 32; st >= 1; st >>= 1) {
-                    const int32_t e = __shfl(excl, j + st, 64);
-                    if (e <= q) j += st;
+                    for (int st = 32; st >= 1; st >>= 1) {
+                        const int32_t e = __shfl(excl, j + st, 64);
+                        if (e <= q) j += st;
+                    }
+                    const int32_t lj = __shfl(lo, j, 64), ej = __shfl(excl, j, 64);
+                    val[u] = q < T;
+                    const size_t in = (size_t)(lj + (q - ej));
+                    pos[u] = !val[u] ? 0 : part ? in : (size_t)(kk + j) * (size_t)max_u + in;
                 }
-                const int32_t lj = __shfl(lo, j, 64), ej = __shfl(excl, j, 64);
-                val[u] = q < T;
-                pos[u] = val[u] ? (size_t)(kk + j) * (size_t)max_u + (size_t)(lj + (q - ej)) : 0;
-            }
-            uint16_t c[kUn];
-            double v[kUn];
+                uint16_t c[kUn];
+                double v[kUn];
+                if (part) {
+                    int32_t r[kUn];
 #pragma unroll
-            for (int u = 0; u < kUn; ++u) {
-                c[u] = fcol16[pos[u]];
-                v[u] = dw[pos[u]];
-            }
+                    for (int u = 0; u < kUn; ++u) {
+                        c[u] = tl.tcol16[pos[u]];
+                        v[u] = tl.tval[pos[u]];
+                        r[u] = tl.trow[pos[u]];
+                    }
 #pragma unroll
-            for (int u = 0; u < kUn; ++u)
-                if (val[u]) atomicAdd(&acc[c[u]], v[u]);
+                    for (int u = 0; u < kUn; ++u) v[u] *= tl.rowcoef[r[u]];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kUn; ++u) {
+                        c[u] = fcol16[pos[u]];
+                        v[u] = dw[pos[u]];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kUn; ++u)
+                    if (val[u]) atomicAdd(&acc[c[u]], v[u]);
+            }
         }
     }
     __syncthreads();
@@ -665,8 +709,13 @@ __global__ __launch_bounds__(256) void fold_finish_kernel(double* tmp, int64_t d
 
 void launch_fold_blocks(const double* dw, const uint16_t* fcol16, const uint32_t* fbnd, const int32_t* items,
                         int32_t n_items, int32_t K, int64_t max_u, int64_t d, double* tmp, double* dw_sum, double* w,
-                        double mult, bool apply, const int32_t* inv, hipStream_t s) {
-    if (n_items > 0) fold_blocks_kernel<<<n_items, 256, 0, s>>>(dw, fcol16, fbnd, items, K, max_u, d, tmp);
+                        double mult, bool apply, const int32_t* inv, hipStream_t s, const FoldTail* tail) {
+    if (n_items > 0) {
+        if (tail)
+            fold_blocks_kernel<true><<<n_items, 256, 0, s>>>(dw, fcol16, fbnd, items, K, max_u, d, tmp, *tail);
+        else
+            fold_blocks_kernel<false><<<n_items, 256, 0, s>>>(dw, fcol16, fbnd, items, K, max_u, d, tmp, FoldTail{});
+    }
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((d + 255) / 256, 4096));
     fold_finish_kernel<<<blocks, 256, 0, s>>>(tmp, d, dw_sum, w, mult, apply ? 1 : 0, inv);
 }

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     }
     if (valid && sub == 0) {  // read once by the solver's loader: nontemporal, like its reads
         __builtin_nontemporal_store(b, a.beg + g);
-        __builtin_nontemporal_store((int32_t)(e - b), a.z + g);
+        __builtin_nontemporal_store(a.row_zs ? a.row_zs[gr] : (int32_t)(e - b), a.z + g);
         __builtin_nontemporal_store(a.y[gr], a.py + g);
         __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
         if (a.xw) __builtin_nontemporal_store(xw, a.xw + g);  // (null: xw_produce_kernel forms x.w)

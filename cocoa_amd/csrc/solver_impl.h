@@ -64,7 +64,7 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
     int64_t beg = 0, z = 0;
     double yv = 0.0, qv = 0.0;
     int32_t fl = 0;
-    double pxw = 0.0;
+    double pxw = 0.0, ppq = 0.0;
     const bool planned = a.plan_beg != nullptr;
     if (valid) {
         const size_t g = (size_t)k * H + s;
@@ -76,6 +76,15 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
             yv = stream_ld(a.plan_y + g);
             qv = stream_ld(a.plan_q + g);
             if (MODE != MODE_COCOA) pxw = stream_ld(a.plan_xw + g);
+            if (MODE == MODE_PLUS && !STRICT && a.row_qp) {
+                // private columns: the row's dot with them is pq (alpha - alpha^0),
+                // alpha^0 folded into x.w here (off the chain)
+                const double qp = a.row_qp[gr];
+                if (qp != 0.0) {
+                    ppq = (yv * qp) * (1.0 / a.lam_n);
+                    pxw -= (a.sigma * ppq) * a.alpha[gr];
+                }
+            }
         } else {
             beg = a.row_ptr[gr];
             z = a.row_ptr[gr + 1] - beg;
@@ -102,6 +111,7 @@ __device__ void load_batch(const SolverArgs& a, int k, int64_t p0, int32_t& curs
         if (!STRICT) {
             const double qii = MODE == MODE_PLUS ? qv * a.sigma : qv;
             mb->rq[lane] = qii != 0.0 ? 1.0 / qii : 0.0;
+            mb->pq[lane] = ppq;
         }
     }
     const int32_t T = __shfl(incl, m - 1, 64);
@@ -406,7 +416,7 @@ struct Chunks3 {
 
 struct Meta3 {
     int32_t r, off, z, fl;    // wave-uniform (SGPRs): control flow and addressing
-    double y, q, rq, xw, aa;  // broadcast LDS reads kept in VGPRs (no readfirstlane wait)
+    double y, q, rq, xw, aa, pq;  // broadcast LDS reads kept in VGPRs (no readfirstlane wait)
 };
 
 // Step metadata and alpha of the sampled row.  alpha is read before the
@@ -422,6 +432,7 @@ __device__ __forceinline__ Meta3 read_meta3(const BatchMeta* mb, int s, const do
     m.q = mb->q[s];
     m.rq = mb->rq[s];
     m.xw = mb->xw[s];
+    m.pq = mb->pq[s];
     m.aa = alv[m.r];
     return m;
 }
@@ -475,7 +486,9 @@ __device__ void compute_batch3(const SolverArgs& a, const BatchMeta* mb, const i
     // CoCoA.scala:159-186 / MinibatchCD.scala:104-123, branch-free
     auto rule = [&](const Meta3& st, double sdot, double& na, double& coef) -> bool {
         const double aa = st.aa;
-        const double grad = MODE == MODE_PLUS ? (st.y * (st.xw + sigma * sdot) - 1.0) * lam_n
+        // (CoCoA+: the private columns' share of x.deltaW is pq aa, st.xw already
+        // holds -sigma pq alpha^0; pq = 0 without private columns)
+        const double grad = MODE == MODE_PLUS ? (st.y * (st.xw + sigma * fma(st.pq, aa, sdot)) - 1.0) * lam_n
                                               : (st.y * st.xw - 1.0) * lam_n;
         const double proj = aa <= 0.0 ? fmin(grad, 0.0) : (aa >= 1.0 ? fmax(grad, 0.0) : grad);
         const bool go = proj != 0.0;
@@ -664,6 +677,10 @@ __global__ __launch_bounds__(128, 1) void solver_kernel(SolverArgs a) {
     } else {
         for (int32_t i = tid; i < nl; i += 128) {
             const double old = a.alpha[p0 + i];
+            // private columns: the row's deltaW per unit of x, y_r (alpha_r - alpha_r^0) /
+            // (lambda n) -- the sum of its updates (CoCoA.scala:181-184) -- for the tail
+            if (!STRICT && MODE == MODE_PLUS && a.rowcoef)
+                a.rowcoef[p0 + i] = (a.y[p0 + i] * (alv[i] - old)) * (1.0 / a.lam_n);
             a.alpha[p0 + i] = old + ((alv[i] - old) * a.scaling);
         }
     }

@@ -331,8 +331,8 @@ class Engine:
         return out.reshape(K, nb * 16, 48)
 
     def plan(self):
-        buf = ctypes.create_string_buffer(1024)
-        C.check(C.lib().cocoa_plan_info(self.h, buf, 1024), self.h)
+        buf = ctypes.create_string_buffer(2048)
+        C.check(C.lib().cocoa_plan_info(self.h, buf, 2048), self.h)
         return json.loads(buf.value.decode())
 
     def sync(self):

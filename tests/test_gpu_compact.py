@@ -129,6 +129,7 @@ def test_block_fold_matches_gather_fold(solver, monkeypatch):
     that zeroes as it reads.  Same rounds, same results within 1e-12 (the
     block fold reassociates the partition sums)."""
     sh = configs.share("c4", n=40000, d=400000, parts=32, n_test=2000)
+    monkeypatch.setenv("COCOA_DW_PRIVATE", "0")  # (the same slot layout in both runs: test_gpu_private.py)
     monkeypatch.setenv("COCOA_DW_DBUF", "0")
     b, eb = run(sh, "cocoa+", True, monkeypatch, rounds=4, solver=solver)
     assert b.plan()["fold"] == "gather" and b.plan()["dw_dbuf"] == 0
@@ -149,6 +150,8 @@ def test_chain_hot_slice_positions_in_lds_are_bitwise_neutral(monkeypatch):
     with COCOA_CHAIN_HOT=0 agree to 1e-12 (the block fold's fp64 atomic adds,
     where work items share a column block, reassociate between runs)."""
     sh = configs.share("c4", n=20000, d=300000, parts=16, n_test=1000)
+    # (the slot per distinct column: with private columns these 16 slices fit LDS whole)
+    monkeypatch.setenv("COCOA_DW_PRIVATE", "0")
     a, ea = run(sh, "cocoa+", True, monkeypatch, rounds=3, solver="chain")
     assert a.plan()["chain_hot"] >= 1024 and a.plan()["vec_lds"] == 0, a.plan()
     monkeypatch.setenv("COCOA_CHAIN_HOT", "0")

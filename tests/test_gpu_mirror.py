@@ -91,3 +91,19 @@ def test_mirror_deferred_eval_trajectory(monkeypatch):
         assert abs(ev["primal"] - rv["primal"]) <= REL * abs(rv["primal"])
         assert abs(ev["gap"] - rv["gap"]) <= REL * abs(rv["primal"])
         assert ev["test_err_count"] == rv["test_err"]
+
+
+@pytest.mark.parametrize("H,on", [(10, 0), (48, 0), (49, 1)])
+def test_mirror_only_past_the_window(H, on, monkeypatch):
+    """The halves first trade partial bases at batch kGNB = 3 (48 steps).  With
+    H <= 48 nothing ties them together, and a half that finished before the
+    other started would overwrite the alphaOld that one still copies in (seen
+    as an intermittent wrong w at H = 10, four members sharing one GPU), so the
+    mirror takes only H > 48; the results match the oracle either way."""
+    tr = configs.share("c2", n=12000, parts=16, n_test=100).train
+    e, plan, _ = _run(monkeypatch, tr, "cocoa+", H, 3, True)
+    assert plan["gram_mirror"] == on, plan
+    run = _oracle(tr, "cocoa+", H, 3)
+    wr = run.w()
+    assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+    assert np.max(np.abs(e.alpha() - run.alpha())) <= REL

@@ -34,7 +34,8 @@ def main():
     # tools/pmc_summary.py [SRC_DIR [TAG [OUT]]]: TAG = the tools/gpu_run.sh TAG of the passes
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out")
     sfx = "_" + sys.argv[2] if len(sys.argv) > 2 else ""
-    f, w = load(os.path.join(src, "pmc_FETCH_SIZE" + sfx)), load(os.path.join(src, "pmc_WRITE_SIZE" + sfx))
+    pre = os.environ.get("PMC_PREFIX", "pmc_")  # (c4pmc_: tools/gpu_run.sh c4pmc)
+    f, w = load(os.path.join(src, pre + "FETCH_SIZE" + sfx)), load(os.path.join(src, pre + "WRITE_SIZE" + sfx))
     cf, cw = load(os.path.join(src, "calib_FETCH_SIZE" + sfx)), load(os.path.join(src, "calib_WRITE_SIZE" + sfx))
     gib = float(1 << 30)
     k_f64 = gib / (pick(cf, "read_f64", "FETCH_SIZE")[0] * 1024)
