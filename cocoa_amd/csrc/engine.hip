@@ -674,6 +674,44 @@ static std::vector<int32_t> fold_items(int64_t nblk, int K, F cnt) {
     return items;
 }
 
+// fold_items with every block's partitions in G contiguous groups, item i of a
+// block covering group i % G and its items interleaved so that item index i
+// runs on XCD i % 8 (round-robin dispatch): with G = 8 each XCD then folds one
+// eighth of the partitions, whose rows' rowcoef (the private tail's gathers)
+// stay in its L2.  Groups with fewer pieces than the block's largest get empty
+// items (k0 = k1: no reads, no stores).
+template <class F>
+static std::vector<int32_t> fold_items_grouped(int64_t nblk, int K, int G, F cnt) {
+    std::vector<int32_t> items;
+    std::vector<std::vector<std::pair<int, int>>> pieces((size_t)G);
+    for (int64_t b = 0; b < nblk; ++b) {
+        size_t most = 0;
+        for (int g = 0; g < G; ++g) {
+            auto& P = pieces[(size_t)g];
+            P.clear();
+            const int ka = (int)((int64_t)K * g / G), kb = (int)((int64_t)K * (g + 1) / G);
+            int64_t acc = 0;
+            int k0 = ka;
+            for (int k = ka; k < kb; ++k) {
+                acc += cnt(b, k);
+                if (acc >= kFoldItem || k == kb - 1) {
+                    P.emplace_back(k0, k + 1);
+                    k0 = k + 1;
+                    acc = 0;
+                }
+            }
+            most = std::max(most, P.size());
+        }
+        for (size_t r = 0; r < most; ++r)
+            for (int g = 0; g < G; ++g) {
+                const auto& P = pieces[(size_t)g];
+                const std::pair<int, int> pc = r < P.size() ? P[r] : std::make_pair(0, 0);
+                items.insert(items.end(), {(int32_t)b, pc.first, pc.second, 0});
+            }
+    }
+    return items;
+}
+
 // Private-column layout (cocoa_ctx::priv_ready; fast mode, COCOA_DW_PRIVATE=0
 // turns it off).  lists[k]: partition k's distinct device columns in device
 // order; pcol / val: the rows as the fast kernels store them.
@@ -768,10 +806,14 @@ static void build_private(cocoa_ctx* c, const int64_t* row_ptr, const int32_t* p
         }
         toff += (int64_t)Tl.size();
     }
-    const std::vector<int32_t> items = fold_items(nblk, K, [&](int64_t b, int k) -> int64_t {
+    auto cnt_bk = [&](int64_t b, int k) -> int64_t {
         return (int64_t)(bnd[(size_t)(b + 1) * K + k] - bnd[(size_t)b * K + k]) +
                (int64_t)(tb[(size_t)(b + 1) * K + k] - tb[(size_t)b * K + k]);
-    });
+    };
+    // (COCOA_FOLD_XCD=0: the plain block-major items, A/B)
+    const char* fx = std::getenv("COCOA_FOLD_XCD");
+    const bool grouped = !(fx && !std::atoi(fx)) && K >= 64;
+    const std::vector<int32_t> items = grouped ? fold_items_grouped(nblk, K, 8, cnt_bk) : fold_items(nblk, K, cnt_bk);
     hipStream_t s = c->stream;
     upload_padded(c->pcol_h, ncol.data(), sizeof(int32_t) * (size_t)nnz, s);
     upload_padded(c->pval_h, nval.data(), sizeof(double) * (size_t)nnz, s);

@@ -22,7 +22,7 @@ def odata(d):
     return oracle.Data(d.row_ptr, d.col, d.val, d.y, d.part_ptr, d.num_features)
 
 
-def _run(tr, te, n_glob, H, lam, private, monkeypatch, rounds=4, seed=3):
+def _run(tr, te, n_glob, H, lam, private, monkeypatch, rounds=4, seed=3, gamma=1.0):
     monkeypatch.setenv("COCOA_DW_COMPACT", "1")
     monkeypatch.setenv("COCOA_DW_PRIVATE", "1" if private else "0")
     e = Engine(strict=False)
@@ -30,7 +30,7 @@ def _run(tr, te, n_glob, H, lam, private, monkeypatch, rounds=4, seed=3):
     if te is not None:
         e.set_test(te)
     e.set_solver("chain")
-    e.init("cocoa+", n_glob, rounds, H, lam, 1.0, 1.0, 1, seed)
+    e.init("cocoa+", n_glob, rounds, H, lam, 1.0, gamma, 1, seed)
     p = e.plan()
     assert p["dw_compact"] == 1 and p["dw_private"] == (1 if private else 0), p
     evs = []
@@ -67,15 +67,16 @@ def test_private_columns_c4_shape_vs_oracle_and_slot_layout(monkeypatch):
         assert abs(x["gap"] - y["gap"]) <= 1e-11 * abs(y["primal"]) and x["test_err_count"] == y["test_err_count"]
 
 
-@pytest.mark.parametrize("H", [150, 1400])
-def test_private_columns_edge_rows_vs_oracle(H, monkeypatch):
+@pytest.mark.parametrize("H,gamma", [(150, 1.0), (1400, 1.0), (600, 0.5)])
+def test_private_columns_edge_rows_vs_oracle(H, gamma, monkeypatch):
     """Empty rows, 5,000-entry rows (read from HBM past the stream buffer),
     duplicate columns (never private: two entries), a one-row partition (every
-    column of it private) and rows sampled many times per round."""
+    column of it private), rows sampled many times per round, and gamma < 1
+    (sigma' = K gamma in the private share, the fold's scaling on the tail)."""
     from tests.test_gpu_gram import _edge
     tr = _edge()
-    e, _ = _run(tr, None, tr.n, H, 2e-3, True, monkeypatch, rounds=4, seed=7)
-    run = oracle.Run(odata(tr), "cocoa+", tr.n, H, 2e-3, 1.0, 1.0, seed=7, nthreads=8)
+    e, _ = _run(tr, None, tr.n, H, 2e-3, True, monkeypatch, rounds=4, seed=7, gamma=gamma)
+    run = oracle.Run(odata(tr), "cocoa+", tr.n, H, 2e-3, 1.0, gamma, seed=7, nthreads=8)
     for t in range(1, 5):
         run.round(t)
     wr = run.w()
