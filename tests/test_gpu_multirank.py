@@ -225,6 +225,7 @@ def _cfg_worker(rank, world, strict, cfg, uid_q, out_q):
         e = Engine(device=0, strict=strict)
         e.set_train(sh.train, part_begin=sh.part_begin, num_parts_global=sh.k_glob)
         e.set_test(sh.test)
+        e.set_solver(cfg.get("solver", "auto"))
         e.comm_init("host", rank, world, uid)
         e.init("cocoa+", sh.n_glob, 4, sh.H, sh.lam)
         plan = e.plan()
@@ -240,6 +241,8 @@ def _cfg_worker(rank, world, strict, cfg, uid_q, out_q):
     (dict(config="c3", n=4096, parts=8, n_test=256), False),
     (dict(config="c4", n=16000, d=200000, parts=8, n_test=400, compact=True), False),
     (dict(config="c4", n=16000, d=200000, parts=8, n_test=400, compact=True), True),
+    # fast CoCoA+ on the chain solver: private columns (test_gpu_private.py) on each rank
+    (dict(config="c4", n=16000, d=200000, parts=8, n_test=400, compact=True, solver="chain"), False),
 ])
 def test_multirank_dense_and_compact_layouts(cfg, strict):
     from cocoa_amd import configs
@@ -259,9 +262,11 @@ def test_multirank_dense_and_compact_layouts(cfg, strict):
     for r in range(world):
         assert not isinstance(out[r], str), out[r]
     want = "dense" if cfg["config"] == "c3" and not strict else ("gram" if not strict else "chain")
-    assert out[0][3]["solver"] == want
+    assert out[0][3]["solver"] == cfg.get("solver", want)
     if cfg.get("compact"):
         assert out[0][3]["dw_compact"] == 1
+    if cfg.get("solver") == "chain" and not strict:
+        assert out[0][3]["dw_private"] == 1 and out[1][3]["dw_private"] == 1
     sh = configs.share(cfg["config"], n=cfg["n"], d=cfg.get("d"), parts=cfg["parts"], n_test=cfg["n_test"],
                        scaling="strong")
     od = oracle.Data(sh.train.row_ptr, sh.train.col, sh.train.val, sh.train.y, sh.train.part_ptr,
