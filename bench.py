@@ -78,6 +78,130 @@ def eval_bytes(tr, te, d, dense):
             + 12 * te.nnz + 8 * (te.n + 1) + 8 * te.n)
 
 
+def comm_mismatch(requested, rank, world, comm):
+    """The error message when the library's communicator (cocoa_comm_info) is not
+    the exchange this run asked for, else None.  An N-rank run must run its deltaW
+    all-reduce over exactly the requested transport with all N ranks: a
+    multi-GPU line that quietly ran over another transport (or fewer ranks) is not
+    a measurement of the path north_star names (CoCoA.scala:45-48 over xGMI)."""
+    if world <= 1:
+        return None
+    if comm is None or comm.get("world") != world or comm.get("rank") != rank:
+        return f"bench.py: rank {rank}/{world} but the library's communicator says {comm}"
+    if comm.get("transport") != requested:
+        return (f"bench.py: --transport {requested} requested with {world} ranks but the library's communicator "
+                f"runs {comm.get('transport')}: refusing to report a line over another exchange")
+    return None
+
+
+def num(v):
+    """v as a float when it is a number (amdsmi returns "N/A" strings for fields a
+    box does not expose), else None."""
+    return float(v) if isinstance(v, (int, float)) and not isinstance(v, bool) else None
+
+
+class GpuTelemetry:
+    """Clocks, power and temperature of this rank's GPU (amdsmi), so that runs on
+    different boxes can be told apart from regressions: snap() reads the current
+    gfx (sclk), memory (mclk) and fabric (fclk) clocks, socket power, the power
+    cap and the hotspot / memory temperatures; start()/stop() sample every 20 ms
+    on a thread for the timed region.  Every read is best effort (a field is None
+    where the box does not expose it)."""
+
+    def __init__(self, bus_id=None, domain_id=None):
+        self.h = None
+        self.samples = []
+        self._thr = None
+        self._stop = False
+        try:
+            import amdsmi
+            self.smi = amdsmi
+            amdsmi.amdsmi_init()
+            hs = amdsmi.amdsmi_get_processor_handles()
+            for h in hs:
+                try:
+                    bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)  # "dddd:bb:dd.f"
+                    dom, bus = int(bdf.split(":")[0], 16), int(bdf.split(":")[1], 16)
+                    if bus_id is None or (bus == bus_id and (domain_id is None or dom == domain_id)):
+                        self.h, self.bdf = h, bdf
+                        break
+                except Exception:
+                    continue
+        except Exception as e:  # no amdsmi / no permission: telemetry stays empty
+            self.err = repr(e)
+
+    def _try(self, f):
+        try:
+            return f()
+        except Exception:
+            return None
+
+    def snap(self):
+        try:
+            return self._snap()
+        except Exception as e:
+            return {"error": repr(e)}
+
+    def _snap(self):
+        if self.h is None:
+            return None
+        smi, h = self.smi, self.h
+        clk = lambda t: num(self._try(lambda: smi.amdsmi_get_clock_info(h, t)["clk"]))  # noqa: E731
+        pw = self._try(lambda: smi.amdsmi_get_power_info(h)) or {}
+        cap = self._try(lambda: smi.amdsmi_get_power_cap_info(h)) or {}
+        temp = lambda t: num(self._try(lambda: smi.amdsmi_get_temp_metric(  # noqa: E731
+            h, t, smi.AmdSmiTemperatureMetric.CURRENT)))
+        gm = self._try(lambda: smi.amdsmi_get_gpu_metrics_info(h)) or {}
+        pick = lambda v: num(v) if num(v) not in (0xFFFF, 0xFFFFFFFF) else None  # noqa: E731
+        return {"t": time.time(),
+                "sclk_mhz": clk(smi.AmdSmiClkType.SYS), "mclk_mhz": clk(smi.AmdSmiClkType.MEM),
+                "fclk_mhz": clk(smi.AmdSmiClkType.DF),
+                "avg_gfxclk_mhz": pick(gm.get("average_gfxclk_frequency")),
+                "power_w": pick(pw.get("current_socket_power")) or pick(pw.get("average_socket_power")),
+                "power_cap_w": (num(cap.get("power_cap")) / 1e6) if num(cap.get("power_cap")) is not None else None,
+                "temp_hotspot_c": temp(smi.AmdSmiTemperatureType.HOTSPOT),
+                "temp_mem_c": temp(smi.AmdSmiTemperatureType.VRAM)}
+
+    def start(self):
+        if self.h is None:
+            return
+        import threading
+        self.samples, self._stop = [], False
+
+        def run():
+            while not self._stop:
+                s = self.snap()
+                if s:
+                    self.samples.append(s)
+                time.sleep(0.02)
+        self._thr = threading.Thread(target=run, daemon=True)
+        self._thr.start()
+
+    def stop(self):
+        if self._thr is not None:
+            self._stop = True
+            self._thr.join(timeout=2)
+            self._thr = None
+        return self.summary()
+
+    def summary(self):
+        try:
+            return self._summary()
+        except Exception as e:  # telemetry never fails the bench
+            return {"error": repr(e)}
+
+    def _summary(self):
+        s = self.samples
+        if not s:
+            return None
+        out = {"samples": len(s)}
+        for k in ("sclk_mhz", "mclk_mhz", "fclk_mhz", "avg_gfxclk_mhz", "power_w", "temp_hotspot_c"):
+            v = [x[k] for x in s if isinstance(x.get(k), (int, float))]
+            if v:
+                out[k] = {"min": min(v), "mean": sum(v) / len(v), "max": max(v)}
+        return out
+
+
 def _free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -190,7 +314,7 @@ def main():
                          f"'bench.py --gpus N' (spawns them) or torch.distributed.run --nproc-per-node N")
     if args.launch_probe:
         if rank == 0:
-            print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank,
+            print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "transport": args.transport,
                               "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}))
         return
     import torch
@@ -224,8 +348,9 @@ def main():
     eng.init(args.method, n_glob, 1 << 30, H, args.lam)
     runner = DistributedCoCoA(eng, transport=args.transport)
     comm = eng.comm_info()  # cocoa_comm_info: the exchange the library itself runs
-    if world > 1 and (comm["world"] != world or comm["rank"] != rank):
-        raise SystemExit(f"bench.py: rank {rank}/{world} but the library's communicator says {comm}")
+    bad = comm_mismatch(args.transport, rank, world, comm)
+    if bad:
+        raise SystemExit(bad)
 
     def barrier():
         eng.sync()  # the engine's own HIP stream
@@ -291,6 +416,10 @@ def main():
             rounds.append(pending)
         return vals, rounds, t
 
+    props = torch.cuda.get_device_properties(local_rank % ndev) if torch.cuda.is_available() else None
+    tele = GpuTelemetry(getattr(props, "pci_bus_id", None), getattr(props, "pci_domain_id", None))
+    tele_before = tele.snap()
+
     t = 1
     _, _, t = steps(t, args.warmup)
     eng.stats_reset()
@@ -300,10 +429,14 @@ def main():
         eng.stats_kernels(["solver", "eval"])
     eng.stats_enable(True)
     barrier()
+    tele_start = tele.snap()
+    tele.start()
     ts = time.perf_counter()
     gaps, timed_rounds, t = steps(t, args.steps)
     barrier()
     dt = max_over_ranks(time.perf_counter() - ts)
+    tele_timed = tele.stop()
+    tele_end = tele.snap()
     stats = eng.kernel_stats()
     # the eval pass alone (in the timed loop it overlaps the next round's solver)
     eng.stats_reset()
@@ -472,6 +605,11 @@ def main():
             "cpu_baseline": cpu,
             "plan": plan,
             "comm": {"transport": comm["transport"] if world > 1 else None, "world": comm["world"] if world > 1 else 1},
+            # the box's clocks / power / temperature (amdsmi): before warmup, at both
+            # ends of the timed region and sampled every 20 ms inside it
+            "gpu_telemetry": {"bdf": getattr(tele, "bdf", None), "before_warmup": tele_before,
+                              "timed_start": tele_start, "timed_end": tele_end, "timed_samples": tele_timed,
+                              "error": getattr(tele, "err", None)},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -124,6 +124,7 @@ SIGNATURES = {
     "cocoa_kernel_stats": (_int, [_vp, _int, _pf64, _pi64]),
     "cocoa_stats_reset": (_int, [_vp]),
     "cocoa_plan_info": (_int, [_vp, ctypes.c_char_p, _int]),
+    "cocoa_gram_fallback_count": (_int, [_vp, ctypes.POINTER(_i32)]),
     "cocoa_debug_gram_rows": (_int, [_vp, _i32, _pf64, _i64]),
     "cocoa_solver_profile": (_int, [_vp, _int]),
     "cocoa_solver_profile_read": (_int, [_vp, ctypes.POINTER(ctypes.c_uint64), _i64]),

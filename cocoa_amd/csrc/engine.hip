@@ -274,6 +274,15 @@ struct cocoa_ctx {
     DevBuf gram_fb[2];
     int gram_chunks = 0;  // > 0: Gram rows by gram_seq_kernel, this many batch runs per partition
     bool gram_mirror = false;  // the Gram solver as two workgroups per partition (solver_gram.h MIRROR)
+    // The mirrored halves of a partition wait on one another, so both must be
+    // resident at once.  On a device this context owns that holds (2 K <= CUs,
+    // pairs dispatched together); on one it shares -- a group member whose
+    // ordinal repeats, ranks on one GPU over the HOST transport -- the other
+    // users' persistent grids could hold every CU while half 0s spin, so the
+    // one-workgroup solver runs instead (decided per launch: a communicator
+    // may be attached after cocoa_init).
+    bool shared_dev = false;   // (cocoa_create_multi: another member has this ordinal)
+    bool device_shared() const;
     int32_t hot_split = 0;     // hot / cold run boundary of the fast-mode rows (COCOA_HOTRUNS)
     DevBuf xbase;              //   their partial-base exchange ([K][4][kXbR][16][2] tagged granules)
     int32_t xtag_epoch = 0;    //   launch counter in the granule tags
@@ -429,6 +438,10 @@ struct cocoa_ctx {
         if (own_stream && stream) (void)hipStreamDestroy(stream);
     }
 };
+
+bool cocoa_ctx::device_shared() const {
+    return shared_dev || (comm && comm->world > 1 && comm->transport == cocoa::kTransportHost);
+}
 
 #define CAPI_BEGIN(ctx)                                             \
     if (!(ctx)) {                                                   \
@@ -1004,6 +1017,17 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     const int64_t nnz = row_ptr[n_rows];
     require(val != nullptr || nnz == 0, COCOA_E_ARG, "cocoa_set_train: null value array");
     ctx->tr_dense = dense_in ? n_rows >= 1 : is_dense(row_ptr, col, n_rows, num_features);
+    // A test set stored for the previous training set is dropped: its columns are
+    // in that set's device feature order and its eval tiles were sized for that d
+    // (eval_tile_entries), so keeping it could evaluate wrong columns or run
+    // 4,096-entry tiles under the 2,048-entry kernel.  Call cocoa_set_test again.
+    if (ctx->has_test) {
+        ctx->has_test = false;
+        ctx->te_dense = false;
+        ctx->te.n = ctx->te.nnz = 0;
+        ctx->n_t_tiles = 0;
+        ctx->n_test_glob = -1;
+    }
     ctx->K_loc = num_parts;
     ctx->K_glob = num_parts_global;
     ctx->part_begin = part_begin;
@@ -1506,7 +1530,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
             // in 27 bits and its links the batch in 18
             {
                 const char* se = std::getenv("COCOA_GRAM_SEQ");
-                const bool seq = !(se && !std::atoi(se)) && ctx->d < ((int64_t)1 << 27) && ctx->nbatch < (1 << 18);
+                const bool seq = !(se && !std::atoi(se)) && gram_seq_supported() && ctx->d < ((int64_t)1 << 27) &&
+                                 ctx->nbatch < (1 << 18);
                 const char* ce = std::getenv("COCOA_GRAM_CHUNKS");
                 // runs per partition: one workgroup per CU on the CUs the solver's K
                 // workgroups leave (C2: 3; r06h A/B beside the solver: 1 run 5.1 ms,
@@ -1523,7 +1548,8 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                 const char* me = std::getenv("COCOA_GRAM_MIRROR");
                 ctx->gram_mirror = !(me && !std::atoi(me)) && 4 * kk <= ncu && !ctx->dw_compact && ctx->row_zc.p &&
                                    (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_COCOA) &&
-                                   ctx->nbatch > gram_window_batches();
+                                   ctx->nbatch > gram_window_batches() &&
+                                   ctx->nbatch < (1 << 20) - 1;  // granule tag: epoch << 20 | (batch + 1)
                 if (ctx->gram_mirror) ctx->xbase.alloc_zero(sizeof(uint64_t) * (size_t)kk * kGramRuns * kXbR * 32, s);
                 else ctx->xbase.free();
                 const int used = (ctx->gram_mirror ? 2 : 1) * kk;
@@ -1582,7 +1608,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         const size_t steps = (size_t)std::max<int64_t>((int64_t)K * H, 1);
         ctx->plan_beg.alloc(steps * sizeof(int64_t));
         ctx->plan_z.alloc(steps * sizeof(int32_t));
-        if (ctx->row_zc.p)
+        if (ctx->row_zc.p || ctx->use_gram)  // (the Gram solver's loader reads the step's look-back there)
             ctx->plan_zc.alloc(steps * 4 * sizeof(int32_t));
         else
             ctx->plan_zc.free();
@@ -1594,7 +1620,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         if (ctx->use_gram && ctx->gt2.p) {  // (the Gram rows' prefetch runs the next plan too)
             ctx->plan_beg2.alloc(steps * sizeof(int64_t));
             ctx->plan_z2.alloc(steps * sizeof(int32_t));
-            if (ctx->row_zc.p)
+            if (ctx->row_zc.p || ctx->use_gram)
                 ctx->plan_zc2.alloc(steps * 4 * sizeof(int32_t));
             else
                 ctx->plan_zc2.free();
@@ -1664,7 +1690,8 @@ static PlanArgs plan_args(cocoa_ctx* c, const int32_t* samples, int set) {
     pa.w = c->w.as<double>();
     pa.steps = (int64_t)c->K_loc * c->P.local_iters;
     pa.H = c->P.local_iters;
-    pa.row_zc = c->plan_zc.p ? c->row_zc.as<int32_t>() : nullptr;
+    pa.row_zc = c->plan_zc.p && c->row_zc.p ? c->row_zc.as<int32_t>() : nullptr;
+    pa.win = c->use_gram && c->plan_zc.p ? 16 * gram_window_batches() : 0;
     pa.row_zs = c->dw_priv ? c->row_zs.as<int32_t>() : nullptr;  // (the chain's rows: shared entries only)
     pa.zc = !c->plan_zc.p ? nullptr : set ? c->plan_zc2.as<int32_t>() : c->plan_zc.as<int32_t>();
     pa.beg = set ? c->plan_beg2.as<int64_t>() : c->plan_beg.as<int64_t>();
@@ -1885,9 +1912,9 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             g.t0 = lsgd_t0;
             g.alpha_work_stride = c->tr.n + K;
             g.hot_split = c->hot_split;
-            g.mirror = c->gram_mirror ? 1 : 0;
+            g.mirror = c->gram_mirror && !c->device_shared() ? 1 : 0;
             g.xbase = c->xbase.as<uint64_t>();
-            if (c->gram_mirror) c->xtag_epoch = (c->xtag_epoch % 4095) + 1;  // 1..4095 (12 tag bits, never 0)
+            if (g.mirror) c->xtag_epoch = (c->xtag_epoch % 4095) + 1;  // 1..4095 (12 tag bits, never 0)
             g.xtag_epoch = c->xtag_epoch;
             const int mode = c->method == COCOA_METHOD_LOCALSGD ? MODE_LSGD : solver_mode(c->method);
             c->timed(COCOA_K_SOLVER, [&] { launch_solver_gram(mode, g, K, s); });
@@ -3004,6 +3031,9 @@ extern "C" int cocoa_create_multi(int32_t n_devices, const int32_t* devices, int
             g->g_ev_rs.push_back(e3);
         }
         g->device = g->subs[0]->device;
+        for (cocoa_ctx* a : g->subs)
+            for (cocoa_ctx* b : g->subs)
+                if (a != b && a->device == b->device) a->shared_dev = true;
         // peer access between distinct devices (xGMI); copies work without it too
         for (cocoa_ctx* a : g->subs)
             for (cocoa_ctx* b : g->subs) {
@@ -3470,23 +3500,15 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
         std::memcpy(buf, p.c_str(), p.size() + 1);
         return COCOA_OK;
     }
-    // windows the last sequential Gram launch sent to the per-window kernel (diagnostic: waits for the side stream)
-    int32_t gfb = -1;
-    if (ctx->use_gram && ctx->gram_chunks > 0 && ctx->gram_fb[0].p) {
-        if (ctx->gstream) HIPCHK(hipStreamSynchronize(ctx->gstream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        int32_t f2[2] = {0, 0};
-        HIPCHK(hipMemcpy(&f2[0], ctx->gram_fb[0].p, sizeof(int32_t), hipMemcpyDeviceToHost));
-        if (ctx->gram_fb[1].p) HIPCHK(hipMemcpy(&f2[1], ctx->gram_fb[1].p, sizeof(int32_t), hipMemcpyDeviceToHost));
-        gfb = std::max(f2[0], f2[1]);  // (the later of the two buffers' launches is not tracked: report the larger)
-    }
-    std::snprintf(buf, (size_t)len,
-                  "{\"gram_chunks\":%d,\"gram_fallback_last\":%d,\"gram_mirror\":%d,\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
+    // (no device access: the call never waits on the streams; the Gram-row
+    // fallback count is cocoa_gram_fallback_count's)
+    const int wrote = std::snprintf(buf, (size_t)len,
+                  "{\"gram_chunks\":%d,\"gram_mirror\":%d,\"strict\":%d,\"method\":%d,\"K_loc\":%d,\"K_glob\":%d,\"d\":%d,\"vec_lds\":%d,\"alpha_lds\":%d,"
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
                   "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d,"
                   "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld}",
-                  ctx->use_gram ? ctx->gram_chunks : 0, gfb, ctx->gram_mirror ? 1 : 0,
+                  ctx->use_gram ? ctx->gram_chunks : 0, ctx->gram_mirror && !ctx->device_shared() ? 1 : 0,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
                   ctx->tr.nnz > 0 ? (double)ctx->n_hot_nnz[(size_t)std::min(ctx->d, 4096)] / (double)ctx->tr.nnz : 0.0,
@@ -3495,5 +3517,26 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
                   ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot, ctx->dw_priv ? 1 : 0,
                   (long long)ctx->max_uh, (long long)ctx->n_tail);
+    require(wrote >= 0 && wrote < len, COCOA_E_ARG, "cocoa_plan_info: buffer too small");
+    CAPI_END(ctx)
+}
+
+// Diagnostic: windows the last sequential Gram launch sent to the per-window
+// kernel (gram_seq_kernel's pool overflows; the larger of the two Gram-row
+// buffers' counts).  Waits for the context's streams.
+extern "C" int cocoa_gram_fallback_count(cocoa_ctx* ctx, int32_t* out) {
+    CAPI_BEGIN(ctx)
+    require(out != nullptr, COCOA_E_ARG, "null output");
+    if (ctx->is_group()) ctx = ctx->subs[0];
+    *out = -1;
+    if (ctx->use_gram && ctx->gram_chunks > 0 && ctx->gram_fb[0].p) {
+        HIPCHK(hipSetDevice(ctx->device));
+        if (ctx->gstream) HIPCHK(hipStreamSynchronize(ctx->gstream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        int32_t f2[2] = {0, 0};
+        HIPCHK(hipMemcpy(&f2[0], ctx->gram_fb[0].p, sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (ctx->gram_fb[1].p) HIPCHK(hipMemcpy(&f2[1], ctx->gram_fb[1].p, sizeof(int32_t), hipMemcpyDeviceToHost));
+        *out = std::max(f2[0], f2[1]);
+    }
     CAPI_END(ctx)
 }

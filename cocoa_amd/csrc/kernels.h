@@ -137,7 +137,9 @@ struct PlanArgs {
     const int32_t* row_zs;    // private columns: per row its shared entries (the step's z), or null
     int64_t* beg;
     int32_t* z;
-    int32_t* zc;              // per step: row_zc of its row, 4 int32 (when row_zc)
+    int32_t* zc;              // per step: 4 int32, the ends of its row's runs 0..2 (row_zc, or all z) and its
+                              // look-back (plan_impl.h), or null
+    int32_t win;              // the Gram solver's window (steps) for the look-back; 0: none
     double* py;
     double* pq;
     double* xw;
@@ -170,7 +172,7 @@ struct GramSolverArgs {
     const int32_t* samples;
     const int64_t* plan_beg;
     const int32_t* plan_z;
-    const int32_t* plan_zc;   // per step: 4 int32, ends of the rows' class runs (row_zc), or null: all class 0
+    const int32_t* plan_zc;   // per step: 4 int32, ends of the rows' runs 0..2 and the step's look-back (PlanArgs)
     const double* plan_y;
     const double* plan_q;
     const double* plan_xw;
@@ -318,6 +320,7 @@ size_t gram_solver_lds(int64_t d, int32_t* hot);
 void launch_gram(const GramArgs& a, hipStream_t s);
 size_t gram_seq_lds();  // LDS bytes of gram_seq_kernel (one workgroup per CU)
 int gram_window_batches();  // batches in the Gram solver's look-back window (kGNB)
+bool gram_seq_supported();  // gram_seq_kernel handles this build's window (kGW)
 void launch_xw_produce(const XwArgs& a, hipStream_t s);
 void launch_xw_gather(const int64_t* part_ptr, const int32_t* samples, int32_t H, int64_t steps,
                       const double* row_xw, double* xw, hipStream_t s);

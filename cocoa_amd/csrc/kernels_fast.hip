@@ -91,6 +91,7 @@ __global__ __launch_bounds__(256) void xw_produce_kernel(XwArgs a) {
 }
 
 int gram_window_batches() { return kGNB; }
+bool gram_seq_supported() { return kGsWindowOK; }
 
 void launch_xw_produce(const XwArgs& a, hipStream_t s) {
     // 4 KB of (unused) LDS: a block then never fits beside a Gram-solver

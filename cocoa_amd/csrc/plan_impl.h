@@ -19,6 +19,16 @@ __host__ __device__ __forceinline__ int plan_threads_per_step(bool strict, const
     return (strict || !a.need_xw || a.xw_cache) ? 1 : 16;
 }
 
+// Look-back of the Gram-window solver's alpha forwarding (solver_gram.h): for
+// step j of a partition, the latest earlier step j' of the same partition with
+// the same sampled row inside j's window [16 floor(j/16) - win, j), or -1.  The
+// step whose alpha update a later step must see before the deltaW it reads
+// (CoCoA.scala:151, 186): the loader marks j' to forward its new alpha to j.
+// Formed here, chip-wide and beside the previous round, instead of by the
+// loader wave's 16-step ballot search (3,500 of its ~10,400 cycles per batch
+// on C2, r08c).  The block's samples and the 63 before them are staged in LDS.
+constexpr int kPlanLook = 79;  // >= win + 15 for every window the solver takes (kGW <= 64)
+
 template <bool STRICT>
 __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     const int tid = threadIdx.x;
@@ -27,6 +37,15 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
     const int sub = tid % per;
     const bool valid = g < a.steps;
     const int64_t gg = valid ? g : 0;
+    __shared__ int32_t sw[256 + kPlanLook];  // samples of steps [gb - kPlanLook, gb + 256 / per)
+    const int64_t gb = (int64_t)blockIdx.x * (256 / per);
+    if (a.win > 0) {
+        for (int i = tid; i < 256 / per + kPlanLook; i += 256) {
+            const int64_t q = gb - kPlanLook + i;
+            sw[i] = (q >= 0 && q < a.steps) ? a.samples[q] : -1;
+        }
+        __syncthreads();
+    }
     const int32_t k = (int32_t)(gg / a.H);
     const int64_t gr = a.part_ptr[k] + a.samples[gg];
     const int64_t b = a.row_ptr[gr], e = a.row_ptr[gr + 1];
@@ -48,9 +67,26 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         __builtin_nontemporal_store(a.y[gr], a.py + g);
         __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
         if (a.xw) __builtin_nontemporal_store(xw, a.xw + g);  // (null: xw_produce_kernel forms x.w)
-        if (a.row_zc) {
+        if (a.zc) {
+            // the ends of the row's column runs 0..2 (all of it in run 0 without row_zc),
+            // and the step's look-back (above) in the fourth word
             typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store(*(const i32x4*)(a.row_zc + 4 * gr), (i32x4*)(a.zc + 4 * g));
+            const int32_t zz = (int32_t)(e - b);
+            i32x4 z4 = a.row_zc ? *(const i32x4*)(a.row_zc + 4 * gr) : i32x4{zz, zz, zz, zz};
+            int32_t prev = -1;
+            if (a.win > 0) {
+                const int32_t j = (int32_t)(g - (int64_t)k * a.H);
+                const int32_t lo = max((j / 16) * 16 - a.win, 0);
+                const int32_t me = a.samples[g];
+                const int iw = (int)(g - gb) + kPlanLook;
+                for (int32_t jp = j - 1; jp >= lo; --jp)
+                    if (sw[iw - (j - jp)] == me) {
+                        prev = jp;
+                        break;
+                    }
+            }
+            z4.w = prev;
+            __builtin_nontemporal_store(z4, (i32x4*)(a.zc + 4 * g));
         }
     }
 }

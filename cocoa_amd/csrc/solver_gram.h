@@ -165,7 +165,7 @@ __device__ __forceinline__ void lgkm_drain() { __builtin_amdgcn_s_waitcnt(0xC07F
 constexpr int kGramTable = 2048;     // hash slots (power of two, 2 x kGramTile)
 constexpr int kGramTile = 1024;      // cold updater entries per hash tile
 constexpr int kGramNU = 8;           // kGramThreads-entry units in registers
-constexpr int kGramWGs = 3;          // workgroups per CU (LDS, and <= 80 VGPRs)
+constexpr int kGramWGs = kGW <= 48 ? 3 : 2;  // workgroups per CU (LDS, and <= 80 VGPRs)
 constexpr int kGramThreads = 512;    // 8 waves
 constexpr int kGramCH = kGramNU * kGramThreads;
 constexpr int kGHotS = kGHot + 1;    // XP row stride (doubles)
@@ -534,11 +534,13 @@ struct GramSeqLds {
 static_assert(sizeof(GramSeqLds) <= 160 * 1024, "gram_seq_kernel LDS");
 static_assert(kGsNU * kGsWaves <= 64, "one lane per (unit, wave) count");
 static_assert(kGsHot % 4 == 0, "MFMA k-steps of 4 hot columns");
-static_assert(kGW == 3 * kGB, "three partner batches (MFMA tiles)");
+// three partner batches (MFMA tiles): other windows (COCOA_GWIN) take gram_kernel
+constexpr bool kGsWindowOK = kGW == 3 * kGB;
 
 typedef double gs_d4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(kGsThreads, 1) void gram_seq_kernel(GramArgs a) {
+  if constexpr (kGsWindowOK) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     GramSeqLds& L = *(GramSeqLds*)lds_raw;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -786,6 +788,7 @@ __global__ __launch_bounds__(kGsThreads, 1) void gram_seq_kernel(GramArgs a) {
     }
     if (a.prof && tid == 0)
         for (int i = 0; i < 7; ++i) atomicAdd((unsigned long long*)&a.prof[i], (unsigned long long)pc[i]);
+  }
 }
 
 // ============================================================== solver ==
@@ -881,7 +884,6 @@ struct GramSolverLds {
     double base[kGramRuns][kGSlots];   // partial base_s per class (mirrored: per run) and slot (memory waves -> chain)
     double part[kGNC][kGB + 1][kGPart];  // memory wave: row partial sums of a batch's products (+ a sink row)
     alignas(16) double gring[kGGt][kGB][kGW];      // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
-    int32_t smpwin[2 * kGSlots];       // loader: sampled row of step p at [p % 128] (look-back window)
     // staged entries (fetch waves -> memory waves), 64 per ring unit: columns, value
     // low words, value high words (the LDS DMA moves 4 bytes a lane), row bytes
     // (0xFF: past the batch's entries).  One address per lane and unit reaches all
@@ -986,8 +988,24 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     const int32_t hot = HOTLDS ? a.hot : 0;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int KP = MIRROR ? (int)(gridDim.x / 2) : (int)gridDim.x;
-    const int k = MIRROR ? (int)(blockIdx.x % (unsigned)KP) : (int)blockIdx.x;
-    const int h = MIRROR ? (int)(blockIdx.x / (unsigned)KP) : 0;  // (same XCD as its pair when K % 8 == 0)
+    // mirrored: block b -> (partition k, half h) with the two halves of a partition
+    // dispatched next to one another and on one XCD (round-robin b % 8): groups of
+    // 8 partitions, b = 16 (k / 8) + 8 h + k % 8; the last, partial group of
+    // r = KP % 8 partitions, b = 16 (KP / 8) + r h + k % 8.  Both halves of a pair
+    // must be resident at once (they wait on each other's bases): a pair is never
+    // split across the dispatch of many other workgroups
+    int k = (int)blockIdx.x, h = 0;
+    if (MIRROR) {
+        const int b = (int)blockIdx.x, full = KP >> 3, G = b >> 4;
+        if (G < full) {
+            h = (b >> 3) & 1;
+            k = 8 * G + (b & 7);
+        } else {
+            const int r = KP & 7, rem = b - 16 * full;
+            h = rem / r;
+            k = 8 * full + rem % r;
+        }
+    }
     // hot columns [0, hotc), column c at hotl[hix(c)].  A mirrored half only
     // touches the columns of its parity (runs h, 2 + h), so its image holds those
     // alone: twice the hot columns in the same LDS (C2: 1,472 -> 2,944, 68% -> 75%
@@ -1025,6 +1043,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     if (tid < kGramRuns) S.cnt[kCBase + tid] = kGNB;
     __syncthreads();
     uint64_t wait_cycles = 0, wait_base_local = 0, wait_base_remote = 0;  // (diagnostics: the chain's base waits)
+    uint64_t wait_load = 0, wait_scat = 0;  // (diagnostics: the chain's waits on the loader / the memory waves' ring)
     uint64_t* pw = a.prof ? &wait_cycles : nullptr;
     const uint64_t t_start = a.prof ? __builtin_readcyclecounter() : 0;
 
@@ -1033,11 +1052,11 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         int32_t cursor[kGNC];  // sub-ring position of the next staged batch, per class
 #pragma unroll
         for (int c = 0; c < kGNC; ++c) cursor[c] = 0;
-        for (int i = lane; i < 2 * kGSlots; i += 64) S.smpwin[i] = -2;
         // the step's inputs one batch ahead (registers)
         const int i = lane & (kGB - 1);
         int32_t xr = nl, xz = 0;
         int32_t xzc[kGramRuns - 1];  // ends of the column runs 0 .. 2 in the row
+        int32_t xpv = -1;            // the step's look-back: latest earlier step of its row in its window (plan)
         double xy = 0.0, xq = 0.0, xxw = 0.0;
         int64_t xbeg = 0;
         double ls = 1.0;   // MODE_LSGD: s before the batch (SGD.scala:119-120), wave-uniform
@@ -1100,6 +1119,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             xz = 0;
 #pragma unroll
             for (int c = 0; c < kGramRuns - 1; ++c) xzc[c] = 0;
+            xpv = -1;
             xy = xq = xxw = 0.0;
             xbeg = 0;
             if (lane < kGB && j < H) {
@@ -1113,11 +1133,24 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 xbeg = a.plan_beg[g0 + j];
                 xz = a.plan_z[g0 + j];
+                typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+                const i32x4 z4 = *(const i32x4*)(a.plan_zc + 4 * (g0 + j));  // (one 16-byte load)
 #pragma unroll
-                for (int c = 0; c < kGramRuns - 1; ++c) xzc[c] = a.plan_zc ? a.plan_zc[4 * (g0 + j) + c] : xz;
+                for (int c = 0; c < kGramRuns - 1; ++c) xzc[c] = z4[c];
+                xpv = z4[3];
             }
         };
         load(0);
+        // (diagnostics: the loader's cycles per phase of an iteration)
+        uint64_t lph[7] = {0, 0, 0, 0, 0, 0, 0};
+        uint64_t ltp = pw ? __builtin_readcyclecounter() : 0;
+        auto lstamp = [&](int i) {
+            if (pw) {
+                const uint64_t t = __builtin_readcyclecounter();
+                lph[i] += t - ltp;
+                ltp = t;
+            }
+        };
         // batch b's records and layouts; the Gram rows of batch b-4 (LDS DMA, their
         // completion published one iteration later: kCLoad = b+1 means records
         // <= b and Gram rows <= b-5 are in LDS)
@@ -1131,11 +1164,16 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             for (int c = 0; c < kGNC; ++c)
                 ok = ok && wait_ge(&S.cnt[kCScat + c], min(b, NB) - kGRing + 1, abortf, a.status, pw);
             if (!ok) break;
-            vm_drain();  // last iteration's loads and DMA
+            {
+                const uint64_t td = pw ? __builtin_readcyclecounter() : 0;
+                vm_drain();  // last iteration's loads and DMA
+                if (pw) wait_base_local += __builtin_readcyclecounter() - td;  // (diagnostics: the loader's drain)
+            }
+            lstamp(0);
             if (b < NB) {
                 const int32_t j = b * kGB + i;
                 const bool valid = lane < kGB && j < H;
-                const int32_t r = xr, z = xz;
+                const int32_t r = xr, z = xz, pv = xpv;
                 // class c: entries [beg + ze[c], beg + ze[c+1]) -- runs 2c, 2c+1, or
                 // (mirrored) run 2c + h
                 int32_t zr[kGramRuns + 1];
@@ -1155,8 +1193,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 const double y = xy, q = xq, xw = xxw;
                 const int64_t beg = xbeg;
                 if (b + 1 < NB) load(b + 1);
-                const int32_t w0 = b * kGB - kGW;  // look-back window: steps [w0, w0 + kGWin)
-                if (MODE != MODE_LSGD && lane < kGB) S.smpwin[j & (2 * kGSlots - 1)] = valid ? r : -2;
+                lstamp(1);
                 // the rows' runs of each class
                 int32_t inc[kGNC], T[kGNC], nu[kGNC];
 #pragma unroll
@@ -1167,21 +1204,9 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                     nu[c] = (T[c] + 63) >> 6;
                 }
                 wave_lds_sync();
-                // previous occurrence of each step's row in the window before it: lanes =
-                // window positions (0..kGW-1: batches b-kGNB .. b-1; kGW + lane: this batch)
-                int32_t pd = -1;
-                if (MODE != MODE_LSGD) {  // (no dual variable to forward in local SGD)
-                    const int32_t ra = lane < kGW ? S.smpwin[(w0 + lane) & (2 * kGSlots - 1)] : -4;
-                    const int32_t rb = valid ? r : -3;
-                    const int32_t m = min(kGB, H - b * kGB);
-                    for (int t = 0; t < m; ++t) {
-                        const int32_t rt = __builtin_amdgcn_readlane(r, t);
-                        const uint64_t mb = __ballot(rb == rt && lane < t);
-                        const uint64_t ma = __ballot(ra == rt);
-                        const int32_t p = mb ? kGW + 63 - __builtin_clzll(mb) : (ma ? 63 - __builtin_clzll(ma) : -1);
-                        if (lane == t) pd = p;
-                    }
-                }
+                lstamp(2);
+                // (each step's previous occurrence in its window: the plan's look-back, pv)
+                lstamp(3);
                 // MODE_LSGD: the step's shrink and s, in step order (SGD.scala:106, 119-120)
                 // on the uniform running s, so every partition forms the same sequence
                 double lB = 0.0, lAE = 0.0, lY = 0.0;
@@ -1228,6 +1253,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                     R.fw = -1;
                     R.fwd = 0;
                 }
+                lstamp(4);
 #pragma unroll
                 for (int c = 0; c < kGNC; ++c) {
                     GLay& L = S.lay[b % kGRing][c];
@@ -1244,12 +1270,13 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                     if (nu[c] <= kGMaxU) cursor[c] += nu[c] * 64;
                 }
                 wave_lds_sync();
-                // mark the earlier occurrence: step w0 + pd forwards its new alpha here
-                if (MODE != MODE_LSGD && lane < kGB && pd >= 0) {
-                    const int32_t js = w0 + pd;
+                // mark the earlier occurrence: step pv forwards its new alpha here
+                if (MODE != MODE_LSGD && valid && pv >= 0) {
+                    const int32_t js = pv;
                     S.rec[((js / kGB) % kGRing) * kGB + (js % kGB)].fw = j & (2 * kGSlots - 1);
                 }
             }
+            lstamp(5);
             const int32_t xg = b - kGGt;  // Gram rows of batch xg: 16 rows x 64 slots
             if (MODE != MODE_MBCD && xg >= 0 && xg < NB) {
                 const uint32_t* src = (const uint32_t*)(gt + (size_t)xg * kGB * kGW);
@@ -1260,7 +1287,10 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             }
             wave_lds_sync();
             if (lane == 0) lds_release(&S.cnt[kCLoad], b + 1);
+            lstamp(6);
         }
+        if (pw && lane == 0 && h == 0)
+            for (int i = 0; i < 7; ++i) a.prof[(size_t)k * kProfStride + 28 + i] = lph[i];
         if (MODE == MODE_LSGD && lane == 0) {  // read after the final barrier
             S.lsgd_s = ls;
             S.lsgd_keep = lkeep;
@@ -1604,14 +1634,14 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                                      : (MIRROR && c != gram_mirror_run(0, h) && c != gram_mirror_run(1, h)) ? &wait_base_remote
                                                                                                                : &wait_base_local))
                         return false;
-                if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw)) return false;
+                if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw ? &wait_load : nullptr)) return false;
             } else if (!wait_ge(&S.cnt[kCLoad], min(g + kGNB + 1, NB), abortf, a.status, pw)) {
                 return false;
             }
             // coefficient ring slot g % kGRing held batch g - kGRing: consumed by both memory waves?
 #pragma unroll
             for (int c = 0; c < kGNC; ++c)
-                if (!wait_ge(&S.cnt[kCScat + c], g - kGRing + 1, abortf, a.status, pw)) return false;
+                if (!wait_ge(&S.cnt[kCScat + c], g - kGRing + 1, abortf, a.status, pw ? &wait_scat : nullptr)) return false;
             if (MODE != MODE_LSGD) {
                 const int32_t g4 = g + kGNB;
                 const GRec& R4 = S.rec[(g4 % kGRing) * kGB + (lane & (kGB - 1))];
@@ -1727,8 +1757,12 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     }
     if (a.prof && lane == 0 && h == 0 && wv < kGWaves) {
         uint64_t* pr = a.prof + (size_t)k * kProfStride + wv * 4;  // [k][64]: waves at 4 wv, memory phases at 48 + 4 c
-        pr[0] = wait_cycles + (role == kRChain ? wait_base_local + wait_base_remote : 0);
+        pr[0] = wait_cycles + (role == kRChain ? wait_base_local + wait_base_remote + wait_load + wait_scat : 0);
         if (role == kRChain) {
+            a.prof[(size_t)k * kProfStride + 40] = wait_load;
+            a.prof[(size_t)k * kProfStride + 41] = wait_scat;
+        }
+        if (role == kRChain || role == kRLoader) {  // (loader: [2] its vm_drain cycles)
             pr[2] = wait_base_local;
             pr[3] = wait_base_remote;
         }

@@ -335,6 +335,12 @@ class Engine:
         C.check(C.lib().cocoa_plan_info(self.h, buf, 2048), self.h)
         return json.loads(buf.value.decode())
 
+    def gram_fallback_count(self):
+        """Windows the last Gram-row launch sent to the per-window kernel (-1: none in use)."""
+        v = ctypes.c_int32(0)
+        C.check(C.lib().cocoa_gram_fallback_count(self.h, ctypes.byref(v)), self.h)
+        return v.value
+
     def sync(self):
         C.check(C.lib().cocoa_sync(self.h), self.h)
 

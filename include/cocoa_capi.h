@@ -169,7 +169,9 @@ int cocoa_comm_ordered_sum(cocoa_comm *comm, double *buf, int64_t n);
 int cocoa_set_train(cocoa_ctx *ctx, int32_t num_parts, const int64_t *part_ptr, const int64_t *row_ptr,
                     const int32_t *col, const double *val, const double *y, int64_t n_rows, int32_t num_features,
                     int32_t part_begin, int32_t num_parts_global);
-/* This rank's share of DebugParams.testData (any row split). */
+/* This rank's share of DebugParams.testData (any row split).  Call it after
+ * cocoa_set_train: cocoa_set_train drops any test set set before it (the test
+ * columns are stored in the training set's device feature order). */
 int cocoa_set_test(cocoa_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *val, const double *y,
                    int64_t n_rows);
 /* Dense variants (epsilon-shaped data, config C3): X is row-major
@@ -323,8 +325,18 @@ int cocoa_stats_reset(cocoa_ctx *ctx);
  * every solver launch while enabled. */
 int cocoa_solver_profile(cocoa_ctx *ctx, int enable);
 int cocoa_solver_profile_read(cocoa_ctx *ctx, uint64_t *out, int64_t count);
-/* Human-readable description of how the solver was planned (LDS placement). */
+/* Human-readable description of how the solver was planned (LDS placement), as
+ * JSON into buf[len]; COCOA_E_ARG if it does not fit.  Touches no device state
+ * (does not wait on the context's streams).  "gram_mirror" is 1 only when the
+ * mirrored Gram solver will run: it assumes a device this context has to itself
+ * (its two workgroups per partition wait on one another), so a group member
+ * whose ordinal repeats or a rank on a HOST-transport communicator runs the
+ * one-workgroup solver. */
 int cocoa_plan_info(cocoa_ctx *ctx, char *buf, int len);
+/* Diagnostics: windows the last Gram-row launch (gram_seq_kernel) handed to the
+ * per-window kernel because its LDS pool overflowed; -1 when that kernel is not
+ * in use.  Synchronises the context. */
+int cocoa_gram_fallback_count(cocoa_ctx *ctx, int32_t *out);
 /* Diagnostics (fast mode, Gram-window solver, not MbCD): the Gram rows of round
  * t's sampled steps (seed = DebugParams.seed + t) as the next cocoa_round(t)
  * would use them, into out[count]: [K_loc][ceil(H/16) * 16][48] doubles, row j

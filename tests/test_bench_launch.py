@@ -55,3 +55,33 @@ def test_bench_two_ranks_host_transport():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["comm"] == {"transport": "host", "world": 2}
     assert d["config"]["K_total"] == 32 and d["value"] > 0
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_under_test", BENCH)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_comm_rule_eight_ranks_must_run_rccl():
+    """an 8-rank line exits non-zero unless the library's
+    communicator runs the requested transport (RCCL) over all 8 ranks."""
+    b = _bench_module()
+    ok = {"transport": "rccl", "rank": 3, "world": 8}
+    assert b.comm_mismatch("rccl", 3, 8, ok) is None
+    assert "runs host" in b.comm_mismatch("rccl", 3, 8, dict(ok, transport="host"))
+    assert b.comm_mismatch("rccl", 3, 8, dict(ok, world=4))
+    assert b.comm_mismatch("rccl", 3, 8, dict(ok, rank=0))
+    assert b.comm_mismatch("rccl", 3, 8, None)
+    assert b.comm_mismatch("rccl", 0, 1, None) is None  # one rank: no exchange
+    assert b.comm_mismatch("host", 1, 2, {"transport": "host", "rank": 1, "world": 2}) is None
+
+
+def test_launch_probe_reports_transport():
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-probe"], cwd=ROOT, env=_clean_env(),
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = _json_lines(p.stdout)[0]
+    assert d["transport"] == "rccl" and d["world"] == 2

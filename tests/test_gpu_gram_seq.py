@@ -33,7 +33,7 @@ def _run(monkeypatch, tr, method, H, T, seq, chunks=None, lam=2e-3):
     e.init(method, tr.n, T, H, lam, 1.0, 1.0, 1, 3)
     for t in range(1, T + 1):
         e.round(t)
-    plan = e.plan()
+    plan = dict(e.plan(), gram_fallback_last=e.gram_fallback_count())
     monkeypatch.delenv("COCOA_GRAM_SEQ")
     monkeypatch.delenv("COCOA_GRAM_CHUNKS", raising=False)
     return e, plan

@@ -107,3 +107,55 @@ def test_mirror_only_past_the_window(H, on, monkeypatch):
     wr = run.w()
     assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
     assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
+
+
+def test_two_c2_contexts_on_one_gpu_mirrored(monkeypatch):
+    """two C2-sized fast contexts sharing the one GPU, both
+    mirrored (each 2 x 64 workgroups), their rounds enqueued back to back so
+    they run concurrently: no hand-off abort, and each matches the oracle.  The
+    halves of a pair are dispatched next to one another (solver_gram.h block
+    numbering), so one context's lone halves cannot hold the CUs its partners
+    (or the other context's) need."""
+    monkeypatch.setenv("COCOA_GRAM_MIRROR", "1")
+    sh = configs.share("c2", n_test=100)
+    tr = sh.train
+    H, T = sh.H, 2
+    engs = []
+    for seed in (5, 6):
+        e = Engine(strict=False)
+        e.set_train(tr)
+        e.set_solver("gram")
+        e.init("cocoa+", tr.n, T, H, 1e-4, 1.0, 1.0, 1, seed)
+        assert e.plan()["gram_mirror"] == 1
+        engs.append(e)
+    for t in range(1, T + 1):
+        for e in engs:
+            e.round(t)  # (enqueued on each context's own stream; nothing waits in between)
+    for e in engs:
+        e.sync()
+    for e, seed in zip(engs, (5, 6)):
+        run = oracle.Run(odata(tr), "cocoa+", tr.n, H, 1e-4, 1.0, 1.0, seed=seed, nthreads=8)
+        for t in range(1, T + 1):
+            run.round(t)
+        wr = run.w()
+        assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
+        assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
+
+
+def test_mirror_off_when_members_share_a_device(monkeypatch):
+    """a group whose members repeat an ordinal shares the device, so
+    the mirrored solver (which needs both halves of every pair resident) is not
+    used there; the result is the oracle's either way."""
+    monkeypatch.setenv("COCOA_GRAM_MIRROR", "1")
+    tr = configs.share("c2", n=48000, parts=16, n_test=100).train
+    H, T = tr.n // 16, 2
+    e = Engine(strict=False, devices=[0, 0])
+    e.set_train(tr)
+    e.set_solver("gram")
+    e.init("cocoa+", tr.n, T, H, 2e-3, 1.0, 1.0, 1, 5)
+    assert e.plan()["gram_mirror"] == 0
+    for t in range(1, T + 1):
+        e.round(t)
+    run = _oracle(tr, "cocoa+", H, T)
+    wr = run.w()
+    assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))

@@ -9,8 +9,12 @@ sys.path.insert(0, ".")
 from cocoa_amd import Engine, configs  # noqa: E402
 
 
+EVAL_FLOW = "--eval" in sys.argv
+
+
 def main():
-    method = sys.argv[1] if len(sys.argv) > 1 else "cocoa+"
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    method = args[0] if args else "cocoa+"
     sh = configs.share("c2")
     e = Engine(strict=False)
     e.set_train(sh.train, part_begin=sh.part_begin, num_parts_global=sh.k_glob)
@@ -19,11 +23,15 @@ def main():
     e.solver_profile(True)
     for t in (1, 2):
         e.round(t)
+        if EVAL_FLOW:
+            e.eval()
     e.sync()
     e.stats_reset()
     e.stats_enable(True)
     for t in (3, 4, 5):
         e.round(t)
+        if EVAL_FLOW:  # the bench's flow: an evaluation behind every round (x.w of the plan from its row cache)
+            e.eval()
     e.sync()
     st = e.kernel_stats()
     S = 64  # kProfStride (kernels.h)
@@ -39,13 +47,20 @@ def main():
     raw = full[:, :24].reshape(e.K_loc, 6, 4)
     roles = ["chain", "loader", "memory0", "memory1", "fetch0", "fetch1"]
     nb = (sh.H + 15) // 16
-    out = {"method": method, "kernel_ms": {k: v["total_ms"] / max(v["launches"], 1) for k, v in st.items()},
+    out = {"method": method, "eval_flow": EVAL_FLOW, "plan": e.plan(), "kernel_ms": {k: v["total_ms"] / max(v["launches"], 1) for k, v in st.items()},
            "waves": {r: {"wait_cyc_mean": float(raw[:, i, 0].mean()), "total_cyc_mean": float(raw[:, i, 1].mean()),
                          "wait_frac": float(raw[:, i, 0].sum() / max(raw[:, i, 1].sum(), 1))}
                      for i, r in enumerate(roles)},
            "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
            "chain_base_wait_frac": {"local": float(raw[:, 0, 2].sum() / max(raw[:, 0, 1].sum(), 1)),
                                     "remote": float(raw[:, 0, 3].sum() / max(raw[:, 0, 1].sum(), 1))},
+           "chain_wait_frac": {"loader": float(full[:, 40].sum() / max(raw[:, 0, 1].sum(), 1)),
+                               "scatter_ring": float(full[:, 41].sum() / max(raw[:, 0, 1].sum(), 1))},
+           "loader_drain_frac": float(raw[:, 1, 2].sum() / max(raw[:, 1, 1].sum(), 1)),
+           "loader_cyc_per_batch": float(raw[:, 1, 1].mean() / nb),
+           "loader_phase_cyc_per_batch": dict(zip(["wait_drain", "load_issue", "scans", "forward_search", "records",
+                                                   "layouts_marks", "gram_dma_release"],
+                                                  (full[:, 28:35].mean(axis=0) / nb).tolist())),
            "memory_phases_cyc_per_batch": {
                "memory%d" % c: dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
                                         (full[:, 48 + 4 * c:52 + 4 * c].mean(axis=0) / nb).tolist()))
