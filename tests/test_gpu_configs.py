@@ -156,6 +156,30 @@ def test_c5_localsgd_fast_gram_solver_vs_oracle(c2):
     assert_state_close(e, run, False)
 
 
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd", "mbsgd", "localsgd"])
+def test_c5_eight_member_context_vs_oracle(c2, method):
+    """BASELINE config 5's 8-GPU split as one 8-member context
+    (cocoa_create_multi): the C2 problem's K = 64 partitions as 8 members x 8
+    partitions, each member its own solver, fold and exchange (the peer-copy
+    reduce-scatter / all-gather: the members repeat ordinal 0 on the one-GPU
+    box, so the mirrored solver is off), 2 rounds of every method against the
+    oracle (MinibatchCD.scala:34-58, SGD.scala:41-67, CoCoA.scala:39-56)."""
+    sh, od, ot = c2
+    sdca = method in ("cocoa+", "cocoa", "mbcd")
+    e = Engine(devices=[0] * 8, strict=False)
+    e.set_train(sh.train)
+    e.set_test(sh.test)
+    e.init(method, sh.n_glob, 2, sh.H, sh.lam)
+    plan = e.plan()
+    assert plan["n_devices"] == 8 and plan["K_loc"] == 8 and plan["gram_mirror"] == 0, plan
+    run = make_run(sh, od, method)
+    for t in (1, 2):
+        e.round(t)
+        run.round(t)
+    assert_close(e.eval(), run.eval(ot), sdca, 2)
+    assert_state_close(e, run, sdca)
+
+
 # ------------------------------------------------------------------ C3 --
 @pytest.fixture(scope="module")
 def c3():
