@@ -271,8 +271,10 @@ def main():
                     help="rank exchange inside libcocoa_hip.so: RCCL over xGMI (one GPU per rank) or HOST (TCP)")
     ap.add_argument("--solver", default="auto", choices=["auto", "gram", "chain", "dense"],
                     help="fast-mode SDCA local solver (cocoa_set_solver)")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # (20 warmup rounds, ~40 ms: the amdsmi telemetry showed the gfx clock still
+    # ramping 1.9 -> 2.1 GHz through a 3-round warmup's timed region)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--strict", action="store_true", help="bit-exact mode (default: fast)")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--d", type=int, default=None)

@@ -1522,6 +1522,26 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
     if (ctx->use_gram) {
         ctx->status.alloc_zero(sizeof(int) * 4, s);
         ctx->nbatch = (H + 15) / 16;  // kGB = 16 steps per batch (solver_gram.h)
+        {
+            // the mirrored solver (COCOA_GRAM_MIRROR=0 turns it off): two workgroups per
+            // partition, each the whole chain and the deltaW columns of one parity, on
+            // 2 K CUs -- 4 K <= CUs when the next round's Gram rows run beside it
+            // (every method but MbCD), 2 K <= CUs for MbCD.  C2 CoCoA+ (r06l, one
+            // box): solver 2.62 -> 2.39 ms; with the plan's look-back (round 6) 2.46
+            // -> 1.79 ms against the one-workgroup solver.  Only past the window's
+            // batches: the halves first trade bases at batch kGNB, and a half
+            // finishing before the other starts would overwrite the alphaOld that
+            // half still copies in (found as an intermittent wrong w at H = 10 with
+            // four members sharing one GPU); MbCD, with no bases to trade, ties them
+            // with a flag (solver_gram.h).
+            const int kk = (int)std::max<int64_t>(K, 1);
+            const char* me = std::getenv("COCOA_GRAM_MIRROR");
+            ctx->gram_mirror = !(me && !std::atoi(me)) && (method == COCOA_METHOD_MBCD ? 2 : 4) * kk <= ncu &&
+                               !ctx->dw_compact && ctx->row_zc.p && ctx->nbatch > gram_window_batches() &&
+                               ctx->nbatch < (1 << 20) - 1;  // granule tag: epoch << 20 | (batch + 1)
+            if (ctx->gram_mirror) ctx->xbase.alloc_zero(sizeof(uint64_t) * (size_t)kk * kGramRuns * kXbR * 32, s);
+            else ctx->xbase.free();
+        }
         if (method != COCOA_METHOD_MBCD) {
             const size_t gtb = sizeof(double) * (size_t)K * (size_t)ctx->nbatch * 16 * 64;
             ctx->gt.alloc(gtb);
@@ -1538,20 +1558,6 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
                 // 2 runs 2.75, 3 runs 1.81, 4 runs 2.72 -- K * 4 = 256 workgroups
                 // need a second pass for the 64 that find no free CU)
                 const int kk = (int)std::max<int64_t>(K, 1);
-                // the mirrored solver (CoCoA+ / CoCoA, 4 K <= CUs; COCOA_GRAM_MIRROR=0 turns it
-                // off): two workgroups per partition, the Gram rows on the rest.  C2 (r06l,
-                // one box): solver 2.62 -> 2.39 ms, step 2.92 -> 2.70
-                // Only past the window's batches: the halves first trade bases at batch
-                // kGNB, and a half finishing before the other starts would overwrite the
-                // alphaOld that half still copies in (found as an intermittent wrong w at
-                // H = 10 with four members sharing one GPU)
-                const char* me = std::getenv("COCOA_GRAM_MIRROR");
-                ctx->gram_mirror = !(me && !std::atoi(me)) && 4 * kk <= ncu && !ctx->dw_compact && ctx->row_zc.p &&
-                                   (method == COCOA_METHOD_COCOA_PLUS || method == COCOA_METHOD_COCOA) &&
-                                   ctx->nbatch > gram_window_batches() &&
-                                   ctx->nbatch < (1 << 20) - 1;  // granule tag: epoch << 20 | (batch + 1)
-                if (ctx->gram_mirror) ctx->xbase.alloc_zero(sizeof(uint64_t) * (size_t)kk * kGramRuns * kXbR * 32, s);
-                else ctx->xbase.free();
                 const int used = (ctx->gram_mirror ? 2 : 1) * kk;
                 const int autoc = std::max(1, std::min(8, (ncu - used) / kk));
                 ctx->gram_chunks = !seq ? 0 : ce ? std::max(1, std::atoi(ce)) : autoc;

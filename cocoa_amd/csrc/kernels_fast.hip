@@ -102,9 +102,9 @@ void launch_xw_produce(const XwArgs& a, hipStream_t s) {
 
 template <int MODE, bool HOTLDS, bool PROJ, int XWM>
 static void launch_sg4(const GramSolverArgs& a, int grid, size_t lds, hipStream_t s) {
-    // the mirrored form (two workgroups per partition): CoCoA+ / CoCoA, hot
-    // columns in LDS; the caller sets a.mirror only then
-    constexpr bool MIR_OK = (MODE == MODE_PLUS || MODE == MODE_COCOA) && HOTLDS;
+    // the mirrored form (two workgroups per partition): hot columns in LDS; the
+    // caller sets a.mirror only then
+    constexpr bool MIR_OK = HOTLDS;
     if (MIR_OK && a.mirror) {
         (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XWM, MIR_OK>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

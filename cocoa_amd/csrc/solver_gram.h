@@ -1042,6 +1042,12 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     __syncthreads();
     if (tid < kGramRuns) S.cnt[kCBase + tid] = kGNB;
     __syncthreads();
+    // MbCD mirrored: no bases tie the halves together, so half 1 flags that it has
+    // copied alphaOld (above; every thread's load has landed, its value stored) and
+    // half 0 waits for the flag before it writes the new alpha (epilogue)
+    uint64_t* const mflag = (MIRROR && MODE == MODE_MBCD) ? a.xbase + (size_t)k * kGramRuns * kXbR * (2 * kGB) : nullptr;
+    const uint64_t mtag = ((uint64_t)(a.xtag_epoch & 0xFFF) << 20) | 0xFFFFFu;
+    if (MIRROR && MODE == MODE_MBCD && h == 1 && tid == 0) __hip_atomic_store(mflag, mtag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t wait_cycles = 0, wait_base_local = 0, wait_base_remote = 0;  // (diagnostics: the chain's base waits)
     uint64_t wait_load = 0, wait_scat = 0;  // (diagnostics: the chain's waits on the loader / the memory waves' ring)
     uint64_t* pw = a.prof ? &wait_cycles : nullptr;
@@ -1773,9 +1779,18 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         // deltaW = w - wInit = s (keep wInit + v) - wInit (SGD.scala:133), the slice
         // holding v (L2: read past L1, like the gathers)
         const double sH = S.lsgd_s, f = S.lsgd_keep ? sH - 1.0 : -1.0;
-        for (int64_t j = tid; j < a.d; j += NTH) {
-            const double v = (HOTLDS && j < hot) ? hotl[j] : dw_load(dwk + j);
-            dwk[j] = fma(sH, v, f * a.w[j]);
+        if (!MIRROR) {
+            for (int64_t j = tid; j < a.d; j += NTH) {
+                const double v = (HOTLDS && j < hot) ? hotl[j] : dw_load(dwk + j);
+                dwk[j] = fma(sH, v, f * a.w[j]);
+            }
+        } else {
+            // mirrored: this half's columns (parity h) only, their hot part in its
+            // image; write-through, the other half writes the interleaved words
+            for (int64_t j = 2 * (int64_t)tid + h; j < a.d; j += 2 * NTH) {
+                const double v = (HOTLDS && j < hotc) ? hotl[hix((int32_t)j)] : dw_load(dwk + j);
+                __hip_atomic_store(dwk + j, fma(sH, v, f * a.w[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         return;
     }
@@ -1794,6 +1809,18 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         }
     }
     if (MIRROR && h != 0) return;  // alpha: the first half's (both hold the same)
+    if (MIRROR && MODE == MODE_MBCD) {  // (half 1 has copied alphaOld: see above)
+        if (tid == 0) {
+            for (uint32_t it = 0; __hip_atomic_load(mflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != mtag; ++it) {
+                if (it > (1u << 24)) {
+                    __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __syncthreads();
+    }
     // alpha = alphaOld + (alpha - alphaOld) * scaling (CoCoA.scala:101, MinibatchCD.scala:127-128)
     if (a.raw_alpha) {
         for (int32_t i = tid; i < nl; i += NTH) a.alpha[p0 + i] = alv[i];

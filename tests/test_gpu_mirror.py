@@ -43,8 +43,10 @@ def _oracle(tr, method, H, T, lam=2e-3, gamma=1.0):
     return run
 
 
-@pytest.mark.parametrize("method", ["cocoa+", "cocoa"])
+@pytest.mark.parametrize("method", ["cocoa+", "cocoa", "mbcd", "localsgd"])
 def test_mirror_c2_rows_match_one_workgroup_and_oracle(method, monkeypatch):
+    """(round 6: MbCD -- no bases, the halves tied by an alphaOld flag -- and
+    local SGD -- MODE_LSGD's epilogue per parity -- mirrored too)"""
     tr = configs.share("c2", n=48000, parts=16, n_test=100).train
     H, T = tr.n // 16, 3
     one, p1, _ = _run(monkeypatch, tr, method, H, T, False)
@@ -54,7 +56,8 @@ def test_mirror_c2_rows_match_one_workgroup_and_oracle(method, monkeypatch):
     wr = run.w()
     for e in (one, two):
         assert np.max(np.abs(e.w() - wr)) <= REL * np.max(np.abs(wr))
-        assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
+        if method != "localsgd":
+            assert np.max(np.abs(e.alpha() - run.alpha())) <= REL
     assert np.max(np.abs(two.w() - one.w())) <= 1e-12 * np.max(np.abs(wr))
 
 
