@@ -332,6 +332,13 @@ struct cocoa_ctx {
     // (eval v4) and reused by the next round's plan; false once w moves
     DevBuf row_xw;
     bool xw_cached = false;
+    // fast mb-SGD in its pull form (kernels.h MbsgdPull): a CSC copy of the rows
+    // (device column order; built by cocoa_init), its tiles, and per-row counts /
+    // coefficients.  csc_ready: built for the current training set.
+    DevBuf csc_ptr, csc_row, csc_val, csc_tiles, row_cnt, row_c;
+    int64_t n_csc_tiles = 0;
+    bool csc_ready = false;
+    bool mbsgd_pull = false;   // this round's mb-SGD runs the pull form
     int32_t max_z = 0;
 
     // stats
@@ -1021,6 +1028,7 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     // in that set's device feature order and its eval tiles were sized for that d
     // (eval_tile_entries), so keeping it could evaluate wrong columns or run
     // 4,096-entry tiles under the 2,048-entry kernel.  Call cocoa_set_test again.
+    ctx->csc_ready = false;  // (the mb-SGD CSC copy is of the old rows)
     if (ctx->has_test) {
         ctx->has_test = false;
         ctx->te_dense = false;
@@ -1340,6 +1348,47 @@ extern "C" int cocoa_set_solver(cocoa_ctx* ctx, int kind) {
     ctx->inited = false;  // takes effect at the next cocoa_init
     for (cocoa_ctx* sub : ctx->subs) sub_check(cocoa_set_solver(sub, kind), sub);
     CAPI_END(ctx)
+}
+
+// The rows as CSC in device column order for the mb-SGD pull (kernels.h
+// MbsgdPull): column offsets are the frequency prefix set_train formed
+// (n_hot_nnz), entries placed by a device fill (rows within a column in
+// arrival order: fast mode), and tiles of <= kPullTile entries -- runs of whole
+// columns, or slices of one longer column.
+static void build_csc(cocoa_ctx* ctx, hipStream_t s) {
+    const int64_t d = ctx->d, nnz = ctx->tr.nnz, n = ctx->tr.n;
+    require((int64_t)ctx->n_hot_nnz.size() == d + 1 && ctx->n_hot_nnz[(size_t)d] == nnz, COCOA_E_STATE,
+            "mb-SGD pull: column counts do not match the training set");
+    ensure_cols(ctx->tr, ctx->d, s);
+    upload(ctx->csc_ptr, ctx->n_hot_nnz.data(), sizeof(int64_t) * (size_t)(d + 1), s);
+    DevBuf cursor;
+    upload(cursor, ctx->n_hot_nnz.data(), sizeof(int64_t) * (size_t)(d + 1), s);
+    ctx->csc_row.alloc(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1));
+    ctx->csc_val.alloc(sizeof(double) * (size_t)std::max<int64_t>(nnz, 1));
+    launch_csc_fill(ctx->tr.row_ptr.as<int64_t>(), ctx->tr.col.as<int32_t>(), ctx->tr.val.as<double>(), n,
+                    cursor.as<int64_t>(), ctx->csc_row.as<int32_t>(), ctx->csc_val.as<double>(), s);
+    std::vector<int64_t> tl;
+    const auto& cp = ctx->n_hot_nnz;
+    int64_t j = 0;
+    while (j < d) {
+        const int64_t len = cp[(size_t)j + 1] - cp[(size_t)j];
+        if (len > kPullTile) {  // a long column: slices
+            for (int64_t e0 = cp[(size_t)j]; e0 < cp[(size_t)j + 1]; e0 += kPullTile)
+                tl.insert(tl.end(), {e0, std::min<int64_t>(e0 + kPullTile, cp[(size_t)j + 1]), j, -1});
+            ++j;
+            continue;
+        }
+        int64_t j1 = j + 1;
+        while (j1 < d && cp[(size_t)j1 + 1] - cp[(size_t)j] <= kPullTile) ++j1;
+        tl.insert(tl.end(), {cp[(size_t)j], cp[(size_t)j1], j, j1});
+        j = j1;
+    }
+    ctx->n_csc_tiles = (int64_t)tl.size() / 4;
+    upload(ctx->csc_tiles, tl.data(), sizeof(int64_t) * std::max<size_t>(tl.size(), 4), s);
+    ctx->row_cnt.alloc_zero(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1), s);
+    ctx->row_c.alloc(sizeof(double) * (size_t)std::max<int64_t>(n, 1));
+    HIPCHK(hipStreamSynchronize(s));  // (cursor is freed on return)
+    ctx->csc_ready = true;
 }
 
 extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const cocoa_debug* debug, int method,
@@ -1667,6 +1716,14 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         ctx->xw_prod = false;
         ctx->xw_flag.free();
     }
+    // fast mb-SGD on CSR rows with dense slices: the pull form (COCOA_MBSGD_PULL=0:
+    // the atomic scatter kernel)
+    {
+        const char* pe = std::getenv("COCOA_MBSGD_PULL");
+        ctx->mbsgd_pull = method == COCOA_METHOD_MBSGD && !ctx->strict && !ctx->tr_dense && !ctx->dw_compact &&
+                          !(pe && !std::atoi(pe)) && ctx->tr.nnz < ((int64_t)1 << 40);
+        if (ctx->mbsgd_pull && !ctx->csc_ready) build_csc(ctx, s);
+    }
     HIPCHK(hipStreamSynchronize(s));
     ctx->inited = true;
     CAPI_END(ctx)
@@ -1985,10 +2042,19 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             // pass through 0 or blow up, which the Gram solver's scalar s does not model)
             const double t0 = lsgd_t0;
             c->timed(COCOA_K_SOLVER, [&] {
-                if (c->strict)
+                if (c->strict) {
                     launch_sgd(local, c->sa, c->P.lambda, t0, K, s);
-                else
+                } else if (!local && c->mbsgd_pull) {
+                    // the round's deltaW as X^T c into slice 0 (device order), folded
+                    // below as one slice
+                    MbsgdPull p{c->csc_ptr.as<int64_t>(), c->csc_row.as<int32_t>(), c->csc_val.as<double>(),
+                                c->csc_tiles.as<int64_t>(), c->n_csc_tiles, c->row_cnt.as<int32_t>(),
+                                c->row_c.as<double>()};
+                    launch_mbsgd_pull(c->sa, p, K, c->tr.n, c->xw_cached ? c->row_xw.as<double>() : nullptr,
+                                      1.0 - (step * c->P.lambda), dws, s);
+                } else {
                     launch_sgd_fast(local, c->sa, c->P.lambda, t0, K, s);
+                }
             });
         }
     } else if (c->method == COCOA_METHOD_MBSGD) {
@@ -2021,9 +2087,9 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         else if (c->dw_compact)
             launch_fold_compact(dws, c->fptr.as<int64_t>(), c->fpos.as<uint32_t>(), d, c->dw_sum, c->w.as<double>(),
                                 c->mult, fuse_apply, c->d_inv.as<int32_t>(), !c->dw_dbuf, s, chain_init);
-        else
-            launch_fold(dws, K, d, c->dw_sum, c->w.as<double>(), c->mult, fuse_apply, c->d_inv.as<int32_t>(),
-                        !c->dw_dbuf, s, chain_init);
+        else  // (the mb-SGD pull leaves the rank's sum in slice 0 alone)
+            launch_fold(dws, c->mbsgd_pull && c->method == COCOA_METHOD_MBSGD && !c->strict ? 1 : K, d, c->dw_sum,
+                        c->w.as<double>(), c->mult, fuse_apply, c->d_inv.as<int32_t>(), !c->dw_dbuf, s, chain_init);
     });
     if (c->dw_dbuf) c->zero_owed = set;
     c->xw_cached = false;  // w moves this round (scale / fused apply / the caller's apply)
@@ -3513,7 +3579,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
                   "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d,"
-                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld}",
+                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld,\"mbsgd_pull\":%d}",
                   ctx->use_gram ? ctx->gram_chunks : 0, ctx->gram_mirror && !ctx->device_shared() ? 1 : 0,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
@@ -3522,7 +3588,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u,
                   !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
                   ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot, ctx->dw_priv ? 1 : 0,
-                  (long long)ctx->max_uh, (long long)ctx->n_tail);
+                  (long long)ctx->max_uh, (long long)ctx->n_tail, ctx->mbsgd_pull ? 1 : 0);
     require(wrote >= 0 && wrote < len, COCOA_E_ARG, "cocoa_plan_info: buffer too small");
     CAPI_END(ctx)
 }

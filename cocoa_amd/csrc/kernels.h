@@ -377,4 +377,27 @@ void launch_row_sqnorm(const int64_t* row_ptr, const double* val, int64_t n, dou
 void launch_sgd(bool local, const SolverArgs& a, double lambda, double t0, int grid, hipStream_t s);
 void launch_sgd_fast(bool local, const SolverArgs& a, double lambda, double t0, int K, hipStream_t s);
 
+// mb-SGD as a transposed SpMV (fast mode, kernels_fast.hip): within a round the
+// driver w is fixed, so the round's deltaW is X^T c with c_r = cnt_r y_r for the
+// rows r whose margin violates (cnt_r = the round's samples of r), summed column
+// by column over a CSC copy of the rows instead of scattered by atomics.
+constexpr int kPullTile = 4096;  // entries per tile of the mb-SGD pull
+struct MbsgdPull {
+    const int64_t* csc_ptr;   // [d + 1] entry offsets per device column
+    const int32_t* csc_row;   // [nnz] rank-local row of each entry
+    const double* csc_val;    // [nnz]
+    const int64_t* tiles;     // [n_tiles][4] (e0, e1, j0, j1): whole columns [j0, j1), or j1 = -1: a slice of j0
+
+    int64_t n_tiles;
+    int32_t* row_cnt;         // [n] samples per row this round (zero on entry)
+    double* row_c;            // [n] c_r
+};
+void launch_csc_fill(const int64_t* row_ptr, const int32_t* col, const double* val, int64_t n_rows, int64_t* cursor,
+                     int32_t* csc_row, double* csc_val, hipStream_t s);
+// out[j] (device order, zero on entry for split columns) = sum over column j of
+// val * c[row]; xw_cache: the rows' x.w before the round's scale (null: formed
+// here from the scaled w)
+void launch_mbsgd_pull(const SolverArgs& a, const MbsgdPull& p, int32_t K, int64_t n_rows, const double* xw_cache,
+                       double scale, double* out, hipStream_t s);
+
 }  // namespace cocoa

@@ -854,6 +854,121 @@ __global__ __launch_bounds__(64) void localsgd_fast_kernel(SolverArgs a, double 
     for (int64_t j = lane; j < d; j += 64) dwk[j] = s * v[j] - a.w[j];  // SGD.scala:133
 }
 
+// ---------------------------------------------- mb-SGD, pull form (C5) --
+// SGD.scala:108-129 with local = false: every sampled step tests its row against
+// the same w (the driver's, scaled by 1 - step lambda at SGD.scala:48-49), and a
+// violator adds x y to deltaW.  Summed over the round, deltaW = sum_r cnt_r y_r
+// [1 - y_r x_r.w > 0] x_r = X^T c.  mbsgd_fast_kernel scatters it with fp64
+// atomics, one per entry of every violating step; atomics execute at the memory
+// side, ~17x slower scattered than streamed (MI355X_MICROARCH.md, global float
+// atomics), and bound that kernel.  Here: the round's sample counts per row,
+// c_r, then every device column's sum of val * c[row] over a CSC copy (built
+// once, cocoa_init), tile by tile: a tile of whole short columns is summed by
+// 16-lane groups from LDS products and stored; a slice of a long column (the
+// frequency order puts them first) is summed by the block and added atomically
+// (a few per long column).  Same terms, another order: fast mode.
+
+// CSC fill: entries of row r to their column's next slot (cursor: csc_ptr copy)
+__global__ __launch_bounds__(256) void csc_fill_kernel(const int64_t* row_ptr, const int32_t* col, const double* val,
+                                                       int64_t n_rows, int64_t* cursor, int32_t* csc_row,
+                                                       double* csc_val) {
+    const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const int sub = threadIdx.x & 15;
+    if (r >= n_rows) return;
+    for (int64_t q = row_ptr[r] + sub; q < row_ptr[r + 1]; q += 16) {
+        const unsigned long long pos = atomicAdd((unsigned long long*)(cursor + col[q]), 1ull);
+        csc_row[pos] = (int32_t)r;
+        csc_val[pos] = val[q];
+    }
+}
+
+void launch_csc_fill(const int64_t* row_ptr, const int32_t* col, const double* val, int64_t n_rows, int64_t* cursor,
+                     int32_t* csc_row, double* csc_val, hipStream_t s) {
+    if (n_rows > 0)
+        csc_fill_kernel<<<(unsigned)((n_rows * 16 + 255) / 256), 256, 0, s>>>(row_ptr, col, val, n_rows, cursor, csc_row,
+                                                                           csc_val);
+}
+
+__global__ __launch_bounds__(256) void mbsgd_count_kernel(const int64_t* part_ptr, const int32_t* samples, int32_t H,
+                                                          int64_t steps, int32_t* cnt) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= steps) return;
+    atomicAdd(cnt + part_ptr[g / H] + samples[g], 1);
+}
+
+// c_r = cnt_r y_r if 1 - y_r x_r.w > 0 (SGD.scala:115, 124), 16 lanes per row;
+// x_r.w = scale * cached (the last evaluation's x.w of the unscaled w) or the
+// dot with the scaled w; cnt_r reset for the next round
+__global__ __launch_bounds__(256) void mbsgd_coef_kernel(const int64_t* row_ptr, const int32_t* col, const double* val,
+                                                         const double* y, const double* w, const double* xw_cache,
+                                                         double scale, int64_t n_rows, int32_t* cnt, double* c) {
+    const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+    const int sub = threadIdx.x & 15;
+    const bool ok = r < n_rows;
+    const int32_t k = ok ? cnt[r] : 0;
+    double xw = 0.0;
+    if (k > 0 && !xw_cache) {
+        double acc = 0.0;
+        for (int64_t q = row_ptr[r] + sub; q < row_ptr[r + 1]; q += 16) acc = fma(val[q], w[col[q]], acc);
+        xw = acc;
+    }
+    if (!xw_cache) xw = row16_sum(xw);  // (whole 16-lane rows: the row sum stays inside them)
+    if (ok && sub == 0) {
+        double cv = 0.0;
+        if (k > 0) {
+            const double yv = y[r];
+            const double d = xw_cache ? scale * xw_cache[r] : xw;
+            if (1.0 - yv * d > 0) cv = (double)k * yv;
+        }
+        c[r] = cv;
+        if (k) cnt[r] = 0;
+    }
+}
+
+// tile t = tiles[4 t .. 4 t + 3] = (e0, e1, j0, j1): entries [e0, e1) holding
+// the whole columns [j0, j1), or with j1 = -1 a slice of column j0 alone, added
+// atomically (its column's out word is zero on entry); <= kPullTile entries
+__global__ __launch_bounds__(256) void mbsgd_pull_kernel(MbsgdPull p, double* out) {
+    __shared__ double prod[kPullTile];
+    __shared__ double red[4];
+    const int tid = threadIdx.x, sub = tid & 15, grp = tid >> 4;
+    for (int64_t t = blockIdx.x; t < p.n_tiles; t += gridDim.x) {
+        const int64_t e0 = p.tiles[4 * t], e1 = p.tiles[4 * t + 1];
+        const int64_t j0 = p.tiles[4 * t + 2], j1 = p.tiles[4 * t + 3];
+        const int n = (int)(e1 - e0);
+        if (j1 < 0) {  // a slice of column j0
+            double acc = 0.0;
+            for (int i = tid; i < n; i += 256) acc = fma(p.csc_val[e0 + i], p.row_c[p.csc_row[e0 + i]], acc);
+            const double s = block_sum_n<256>(acc, red);
+            if (tid == 0) unsafeAtomicAdd(out + j0, s);
+            __syncthreads();
+            continue;
+        }
+        for (int i = tid; i < n; i += 256) prod[i] = p.csc_val[e0 + i] * p.row_c[p.csc_row[e0 + i]];
+        __syncthreads();
+        for (int64_t j = j0 + grp; j < j1; j += 16) {
+            const int b = (int)(p.csc_ptr[j] - e0), e = (int)(p.csc_ptr[j + 1] - e0);
+            double acc = 0.0;
+            for (int q = b + sub; q < e; q += 16) acc += prod[q];
+            const double s = row16_sum(acc);
+            if (sub == 0) out[j] = s;
+        }
+        __syncthreads();
+    }
+}
+
+void launch_mbsgd_pull(const SolverArgs& a, const MbsgdPull& p, int32_t K, int64_t n_rows, const double* xw_cache,
+                       double scale, double* out, hipStream_t s) {
+    const int64_t steps = (int64_t)K * a.H;
+    if (steps > 0)
+        mbsgd_count_kernel<<<(unsigned)((steps + 255) / 256), 256, 0, s>>>(a.part_ptr, a.samples, a.H, steps, p.row_cnt);
+    if (n_rows > 0)
+        mbsgd_coef_kernel<<<(unsigned)((n_rows * 16 + 255) / 256), 256, 0, s>>>(a.row_ptr, a.col, a.val, a.y, a.w, xw_cache,
+                                                                              scale, n_rows, p.row_cnt, p.row_c);
+    if (p.n_tiles > 0)
+        mbsgd_pull_kernel<<<(unsigned)std::min<int64_t>(p.n_tiles, 2048), 256, 0, s>>>(p, out);
+}
+
 void launch_sgd_fast(bool local, const SolverArgs& a, double lambda, double t0, int K, hipStream_t s) {
     if (local) {
         localsgd_fast_kernel<<<K, 64, 0, s>>>(a, lambda, t0);
