@@ -335,6 +335,13 @@ struct cocoa_ctx {
     // fast mb-SGD in its pull form (kernels.h MbsgdPull): a CSC copy of the rows
     // (device column order; built by cocoa_init), its tiles, and per-row counts /
     // coefficients.  csc_ready: built for the current training set.
+    // fast evaluation split by column (EvalArgs::row_base): the train rows'
+    // entries in device columns < kEvalHot (hot CSR, 16-bit columns) and the rest
+    // (cold CSR), with tiles for each, and the hot pass's per-row dots
+    Csr hot_tr, cold_tr;
+    DevBuf hot_tiles, cold_tiles, row_base;
+    int64_t n_hot_tiles = 0, n_cold_tiles = 0;
+    bool split_ready = false;
     DevBuf csc_ptr, csc_row, csc_val, csc_tiles, row_cnt, row_c;
     int64_t n_csc_tiles = 0;
     bool csc_ready = false;
@@ -1008,6 +1015,60 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
 }
 
 // dense_in: dense rows (row r = columns 0..d-1 at entries [r d, (r+1) d), col unused)
+// The fast evaluation's hot / cold split of the train rows (EvalArgs::row_base):
+// entries of device columns < kEvalHot into one CSR (16-bit columns), the rest
+// into another, each row's entries in stored order, and eval tiles for both.
+// COCOA_EVAL_SPLIT=0 keeps the one-pass evaluation.
+static void build_eval_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::vector<int32_t>& pcol,
+                             const double* val, int64_t n, int32_t d, hipStream_t s) {
+    const char* se = std::getenv("COCOA_EVAL_SPLIT");
+    ctx->split_ready = false;
+    ctx->hot_tr = Csr{};
+    ctx->cold_tr = Csr{};
+    if ((se && !std::atoi(se)) || ctx->strict || n < 1) return;
+    std::vector<int64_t> hp((size_t)n + 1), cp((size_t)n + 1);
+    hp[0] = cp[0] = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t h = 0;
+        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) h += pcol[(size_t)q] < kEvalHot;
+        hp[(size_t)r + 1] = hp[(size_t)r] + h;
+        cp[(size_t)r + 1] = cp[(size_t)r] + (row_ptr[r + 1] - row_ptr[r] - h);
+    }
+    const int64_t nh = hp[(size_t)n], nc = cp[(size_t)n];
+    std::vector<uint16_t> hc((size_t)std::max<int64_t>(nh, 1));
+    std::vector<double> hv((size_t)std::max<int64_t>(nh, 1)), cv((size_t)std::max<int64_t>(nc, 1));
+    std::vector<int32_t> cc((size_t)std::max<int64_t>(nc, 1));
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t a = hp[(size_t)r], b = cp[(size_t)r];
+        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) {
+            const int32_t c = pcol[(size_t)q];
+            if (c < kEvalHot) {
+                hc[(size_t)a] = (uint16_t)c;
+                hv[(size_t)a++] = val[q];
+            } else {
+                cc[(size_t)b] = c;
+                cv[(size_t)b++] = val[q];
+            }
+        }
+    }
+    ctx->hot_tr.n = ctx->cold_tr.n = n;
+    ctx->hot_tr.nnz = nh;
+    ctx->cold_tr.nnz = nc;
+    upload(ctx->hot_tr.row_ptr, hp.data(), sizeof(int64_t) * (size_t)(n + 1), s);
+    upload_padded(ctx->hot_tr.col16, hc.data(), sizeof(uint16_t) * (size_t)nh, s);
+    upload_padded(ctx->hot_tr.val, hv.data(), sizeof(double) * (size_t)nh, s);
+    upload(ctx->cold_tr.row_ptr, cp.data(), sizeof(int64_t) * (size_t)(n + 1), s);
+    upload_padded(ctx->cold_tr.col, cc.data(), sizeof(int32_t) * (size_t)nc, s);
+    upload_col16(ctx->cold_tr.col16, cc, nc, d, s);  // (synchronises: the host vectors may go)
+    upload_padded(ctx->cold_tr.val, cv.data(), sizeof(double) * (size_t)nc, s);
+    int hcap = kEvalTile, ccap = kEvalTile;
+    eval_split_tiles(&hcap, &ccap);
+    ctx->n_hot_tiles = make_tiles(hp.data(), n, ctx->hot_tiles, s, hcap);    // (synchronises)
+    ctx->n_cold_tiles = make_tiles(cp.data(), n, ctx->cold_tiles, s, ccap);
+    ctx->row_base.alloc(sizeof(double) * (size_t)n);
+    ctx->split_ready = true;
+}
+
 static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, const int64_t* part_ptr,
                            const int64_t* row_ptr, const int32_t* col, const double* val, const double* y,
                            int64_t n_rows, int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
@@ -1175,6 +1236,10 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     upload(ctx->rowflags, fl.data(), (size_t)n_rows, s);
     upload(ctx->part_ptr, part_ptr, sizeof(int64_t) * (size_t)(num_parts + 1), s);
     ctx->n_tiles = make_tiles(row_ptr, n_rows, ctx->tiles, s, eval_tile_entries(num_features));
+    if (!dense_in && !ctx->tr_dense)
+        build_eval_split(ctx, row_ptr, pcol, split_classes ? pval.data() : val, n_rows, num_features, s);
+    else
+        ctx->split_ready = false;
     if (dense_in) {
         ctx->compact_ready = false;  // dense rows touch every column: no compact slices
         ctx->priv_ready = false;
@@ -2349,6 +2414,21 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
     e.n_tiles = ctx->n_tiles;
     e.t_tiles = ctx->has_test ? ctx->t_tiles.as<int64_t>() : nullptr;
     e.n_t_tiles = ctx->has_test ? ctx->n_t_tiles : 0;
+    if (!ctx->strict && !dense_eval && ctx->split_ready) {
+        // the split evaluation: hot pass, then the cold entries in place of the rows
+        e.h_row_ptr = ctx->hot_tr.row_ptr.as<int64_t>();
+        e.h_col16 = ctx->hot_tr.col16.as<uint16_t>();
+        e.h_val = ctx->hot_tr.val.as<double>();
+        e.h_tiles = ctx->hot_tiles.as<int64_t>();
+        e.n_h_tiles = ctx->n_hot_tiles;
+        e.row_base = ctx->row_base.as<double>();
+        e.row_ptr = ctx->cold_tr.row_ptr.as<int64_t>();
+        e.col = ctx->cold_tr.col.as<int32_t>();
+        e.col16 = ctx->cold_tr.col16.p ? ctx->cold_tr.col16.as<uint16_t>() : nullptr;
+        e.val = ctx->cold_tr.val.as<double>();
+        e.tiles = ctx->cold_tiles.as<int64_t>();
+        e.n_tiles = ctx->n_cold_tiles;
+    }
     ctx->timed_on(st, COCOA_K_EVAL, [&] {
         if (ctx->strict)
             launch_eval_strict(e, st);

@@ -299,7 +299,19 @@ struct EvalArgs {
     // pass evaluates, stream order) copied to status_host (pinned), or null
     const int* status;
     int* status_host;
+    // hot / cold split of the train rows (cocoa_ctx::split_ready, fast mode), or
+    // row_base null: the hot entries (device column < kEvalHot) as their own CSR
+    // with 16-bit columns and tiles; row_ptr / col / col16 / val / tiles above
+    // then hold the cold entries, and row_base [n] the hot pass's row dots
+    const int64_t* h_row_ptr;
+    const uint16_t* h_col16;
+    const double* h_val;
+    const int64_t* h_tiles;
+    int64_t n_h_tiles;
+    double* row_base;
 };
+constexpr int kEvalHot = 4096;  // w columns in LDS in the split evaluation's hot pass
+void eval_split_tiles(int* hot_cap, int* cold_cap);  // tile entries of its hot / cold passes
 
 // fast translation unit
 void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs& a, int grid, size_t lds,

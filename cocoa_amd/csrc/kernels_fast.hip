@@ -279,7 +279,9 @@ __device__ __forceinline__ void eval_reduce(const double* partials, int blocks, 
     }
 }
 
-template <int TILE, int BLOCK, bool C16, int DIAGW = 0, int HOT = 0>
+// BASE: the train rows' dot starts from row_base[r] (the hot pass below: the
+// pass then streams the cold part of a hot / cold split, cocoa_ctx::split_ready)
+template <int TILE, int BLOCK, bool C16, int DIAGW = 0, int HOT = 0, bool BASE = false>
 __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     constexpr int UNITS = TILE / (4 * BLOCK);  // 4-entry units per thread (base alignment adds one)
     __shared__ double prod[TILE + 4];
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
         if (T > TILE) {
             double acc = 0.0;
             for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += vl[q] * a.w[cl[q]];
-            const double dot = block_sum_n<BLOCK>(acc, red);
+            const double dot = block_sum_n<BLOCK>(acc, red) + ((BASE && !test) ? a.row_base[r0] : 0.0);
             if (tid == 0) {
                 if (!test) {
                     hinge += jmax(1 - yy[r0] * dot, 0.0);
@@ -357,9 +359,10 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             const int b = roff[r] + sh, e = roff[r + 1] + sh;
             double acc = 0.0;
             for (int q = b + sub; q < e; q += 16) acc += prod[q];
-            const double dot = row16_sum(acc);
+            double dot = row16_sum(acc);
             if (sub == 0) {
                 if (!test) {
+                    if (BASE) dot += a.row_base[r0 + r];
                     hinge += jmax(1 - yy[r0 + r] * dot, 0.0);
                     if (a.row_xw) a.row_xw[r0 + r] = dot;
                 } else {
@@ -576,7 +579,121 @@ static bool launch_eval_diag(const EvalArgs& a, bool c16, hipStream_t s) {
 int eval_tile_entries(int64_t d) { return d > kEvalWideD ? 2048 : kEvalTile; }
 #endif
 
+// Hot pass of the split evaluation (cocoa_ctx::split_ready): the train rows'
+// entries in device columns < HOT -- the most frequent: C2 78%, C4 72% of the
+// entries at 4,096 -- as their own CSR with 16-bit columns, w's first HOT
+// columns in LDS, so the pass issues no global gather at all (the texture
+// addresser's per-instruction cost bounds the one-pass kernel, DESIGN.md section
+// 3.3); each row's partial dot goes to row_base.  The cold pass
+// (eval_stream_kernel<..., BASE>) then streams the remaining entries with global
+// gathers, adds row_base and does the hinge / error / alpha / ||w|| sums.  Tiles
+// and loads as in eval_stream_kernel.
+template <int TILE, int BLOCK, int HOT>
+__global__ __launch_bounds__(BLOCK) void eval_hot_kernel(EvalArgs a) {
+    constexpr int UNITS = TILE / (4 * BLOCK);
+    __shared__ double prod[TILE + 4];
+    __shared__ uint16_t roff[TILE + 2];
+    __shared__ double red[BLOCK / 64];
+    __shared__ double whot[HOT];
+    const int tid = threadIdx.x;
+    {
+        const int32_t h = (int32_t)min<int64_t>(HOT, a.d);
+        for (int32_t j = tid; j < HOT; j += BLOCK) whot[j] = j < h ? a.w[j] : 0.0;
+        __syncthreads();
+    }
+    const int sub = tid & 15, grp = tid >> 4;
+    const int64_t* tl = a.h_tiles;
+    const int64_t* te = tl + a.n_h_tiles + 1;
+    const int64_t* rp = a.h_row_ptr;
+    const uint16_t* cl = a.h_col16;
+    const double* vl = a.h_val;
+    for (int64_t t = blockIdx.x; t < a.n_h_tiles; t += gridDim.x) {
+        const int64_t r0 = tl[t], r1 = tl[t + 1];
+        const int64_t e0 = te[t], e1 = te[t + 1];
+        const int64_t T = e1 - e0;
+        if (T > TILE) {
+            double acc = 0.0;
+            for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += vl[q] * whot[cl[q]];
+            const double dot = block_sum_n<BLOCK>(acc, red);
+            if (tid == 0) a.row_base[r0] = dot;
+            continue;
+        }
+        const int nr = (int)(r1 - r0);
+        for (int i = tid; i <= nr; i += BLOCK) roff[i] = (uint16_t)(rp[r0 + i] - e0);
+        const int64_t base = e0 & ~(int64_t)3;
+        const int sh = (int)(e0 - base);
+        const int64_t span = e1 - base;
+        i32x4 c[UNITS + 1];
+        f64x2 v0[UNITS + 1], v1[UNITS + 1];
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            c[u] = i32x4{0, 0, 0, 0};
+            v0[u] = f64x2{0.0, 0.0};
+            v1[u] = v0[u];
+            if (k < span) {
+                c[u] = load_cols<true>(nullptr, cl, base + k);
+                v0[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k));
+                v1[u] = __builtin_nontemporal_load((const f64x2*)(vl + base + k + 2));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u <= UNITS; ++u) {
+            const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
+            if (k < span) {
+                *(f64x2*)(prod + k) = f64x2{v0[u].x * whot[c[u].x], v0[u].y * whot[c[u].y]};
+                *(f64x2*)(prod + k + 2) = f64x2{v1[u].x * whot[c[u].z], v1[u].y * whot[c[u].w]};
+            }
+        }
+        __syncthreads();
+        for (int r = grp; r < nr; r += BLOCK / 16) {
+            const int b = roff[r] + sh, e = roff[r + 1] + sh;
+            double acc = 0.0;
+            for (int q = b + sub; q < e; q += 16) acc += prod[q];
+            const double dot = row16_sum(acc);
+            if (sub == 0) a.row_base[r0 + r] = dot;
+        }
+        __syncthreads();
+    }
+}
+
+// tile entries and block threads of the two passes (A/B knobs: make variant DEFS=...)
+#ifndef COCOA_HOT_TILE
+#define COCOA_HOT_TILE 4096
+#endif
+#ifndef COCOA_HOT_BLOCK
+#define COCOA_HOT_BLOCK 1024  // (C2, one box: 512 threads 0.213 ms for both passes, 1,024 0.205; 2,048-entry tiles 0.216 / 0.233)
+#endif
+#ifndef COCOA_HOT_WGS
+#define COCOA_HOT_WGS 2  // workgroups per CU the hot pass launches
+#endif
+#ifndef COCOA_COLD_TILE
+#define COCOA_COLD_TILE 4096
+#endif
+#ifndef COCOA_COLD_BLOCK
+#define COCOA_COLD_BLOCK 512
+#endif
+void eval_split_tiles(int* hot_cap, int* cold_cap) {
+    *hot_cap = COCOA_HOT_TILE;
+    *cold_cap = COCOA_COLD_TILE;
+}
+
+// the split evaluation: hot pass, then the cold pass over a's (cold) train CSR
+// and the (unsplit) test rows
+static bool launch_eval_split(const EvalArgs& a, int blocks, hipStream_t s) {
+    const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
+    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_h_tiles, 256 * COCOA_HOT_WGS));
+    eval_hot_kernel<COCOA_HOT_TILE, COCOA_HOT_BLOCK, kEvalHot><<<hb, COCOA_HOT_BLOCK, 0, s>>>(a);
+    if (c16)
+        eval_stream_kernel<COCOA_COLD_TILE, COCOA_COLD_BLOCK, true, 0, 0, true><<<blocks, COCOA_COLD_BLOCK, 0, s>>>(a);
+    else
+        eval_stream_kernel<COCOA_COLD_TILE, COCOA_COLD_BLOCK, false, 0, 0, true><<<blocks, COCOA_COLD_BLOCK, 0, s>>>(a);
+    if (!a.counter) eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
+    return a.counter && a.out_host;
+}
+
 bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
+    if (a.row_base) return launch_eval_split(a, blocks, s);
     const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
 #ifdef COCOA_DIAG
     EvalArgs u = a;

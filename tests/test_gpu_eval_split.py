@@ -1,0 +1,101 @@
+"""The split evaluation (kernels_fast.hip eval_hot_kernel + eval_stream_kernel
+BASE; cocoa_ctx::split_ready): the train rows' entries in the 4,096 most
+frequent device columns are summed by a hot pass with w in LDS and no global
+gather, the rest by the cold pass, which adds the hot dots and forms the
+hinge / alpha / ||w|| / test-error sums (OptUtils.scala:57-98).  Checked
+against the oracle and the one-pass evaluation (COCOA_EVAL_SPLIT=0) on the same
+(w, alpha): C2 and C4-shaped rows (16-bit and 32-bit cold columns), rows longer
+than a tile in either part (a 5,000-entry row of duplicate hot columns), empty
+rows, and the next round's plan reading the x.w it stored."""
+import numpy as np
+import pytest
+
+from cocoa_amd import Engine, LabeledData, configs
+from oracle import oracle
+from tests.test_gpu_parity import _eval_edge_data
+
+pytestmark = pytest.mark.gpu
+
+
+def odata(d):
+    return oracle.Data(d.row_ptr, d.col, d.val, d.y, d.part_ptr, d.num_features)
+
+
+def _state(tr, H, lam, rounds=3):
+    run = oracle.Run(odata(tr), "cocoa+", tr.n, H, lam, seed=3, nthreads=16)
+    for t in range(1, rounds + 1):
+        run.round(t)
+    return run
+
+
+def _eval(monkeypatch, tr, te, run, H, lam, split):
+    monkeypatch.setenv("COCOA_EVAL_SPLIT", "1" if split else "0")
+    e = Engine(strict=False)
+    e.set_train(tr)
+    monkeypatch.delenv("COCOA_EVAL_SPLIT")
+    e.set_test(te)
+    e.init("cocoa+", tr.n, 0, H, lam)
+    e.set_w(run.w())
+    e.set_alpha(run.alpha())
+    return e, e.eval()
+
+
+def _check(ev, rv, tol):
+    for k in ("primal", "dual", "gap"):
+        assert abs(ev[k] - rv[k]) <= tol * abs(rv["primal"]), (k, ev[k], rv[k])
+    assert ev["test_err_count"] == rv["test_err"]
+
+
+def _dup_rows():
+    """Edge rows plus a 5,000-entry row over 60 hot columns (duplicates): its hot
+    part alone passes the 4,096-entry tile."""
+    tr = _eval_edge_data()
+    rng = np.random.default_rng(4)
+    cols = rng.integers(0, 60, size=5000).astype(np.int32)
+    vals = rng.standard_normal(5000) / 70.0
+    row_ptr = np.concatenate([tr.row_ptr, [tr.row_ptr[-1] + 5000]]).astype(np.int64)
+    part = tr.part_ptr.copy()
+    part[-1] += 1
+    return LabeledData(row_ptr, np.concatenate([tr.col, cols]), np.concatenate([tr.val, vals]),
+                       np.concatenate([tr.y, [1.0]]), part, tr.num_features)
+
+
+@pytest.mark.parametrize("data", ["c2", "c4", "edge"])
+def test_split_eval_matches_oracle_and_one_pass(data, monkeypatch):
+    if data == "edge":
+        tr = _dup_rows()
+        te = tr.row_range(200, 1300)
+        H, lam = 200, 2e-3
+    else:
+        sh = configs.share(data, n=60000 if data == "c2" else 40000, parts=16, n_test=3000)
+        tr, te = sh.train, sh.test
+        H, lam = sh.H, 1e-4
+    run = _state(tr, H, lam)
+    rv = run.eval(odata(te))
+    e1, ev1 = _eval(monkeypatch, tr, te, run, H, lam, True)
+    e0, ev0 = _eval(monkeypatch, tr, te, run, H, lam, False)
+    _check(ev1, rv, 1e-12)
+    _check(ev0, rv, 1e-12)
+    for k in ("primal", "dual", "gap"):
+        assert abs(ev1[k] - ev0[k]) <= 1e-13 * abs(rv["primal"])
+
+
+def test_split_eval_xw_feeds_the_next_round(monkeypatch):
+    """The cold pass stores each row's full x.w (hot + cold); the next round's
+    plan takes x.w from it: CoCoA+ rounds with an evaluation after each stay
+    within 1e-9 of the oracle."""
+    sh = configs.share("c2", n=48000, parts=16, n_test=2000)
+    tr, te = sh.train, sh.test
+    H = sh.H
+    e = Engine(strict=False)
+    e.set_train(tr)
+    e.set_test(te)
+    e.init("cocoa+", tr.n, 6, H, 1e-4, 1.0, 1.0, 1, 5)
+    run = oracle.Run(odata(tr), "cocoa+", tr.n, H, 1e-4, 1.0, 1.0, seed=5, nthreads=16)
+    ot = odata(te)
+    for t in range(1, 7):
+        e.round(t)
+        run.round(t)
+        _check(e.eval(), run.eval(ot), 1e-9)
+    wr = run.w()
+    assert np.max(np.abs(e.w() - wr)) <= 1e-9 * np.max(np.abs(wr))
