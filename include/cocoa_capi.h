@@ -191,8 +191,13 @@ int cocoa_set_test_dense(cocoa_ctx *ctx, const double *X, const double *y, int64
 /* Local solver of the SDCA methods in fast mode (strict mode always runs the
  * chain solver, which sums every dot in the reference's order):
  *   CHAIN -- each step gathers deltaW (or w) at its row and reduces the dot;
- *   GRAM  -- the dot is a lagged gather plus Gram corrections of the last 64
- *            steps, so the sequential chain does no memory access;
+ *   GRAM  -- the dot is a lagged gather plus Gram corrections of the last 48
+ *            steps, so the sequential chain does no memory access.  With
+ *            2 K (MbCD) or 4 K (the others) <= CUs it runs mirrored: two
+ *            workgroups per partition that wait on each other, so it assumes a
+ *            device this context has to itself (a group member whose ordinal
+ *            repeats, or a rank on a HOST-transport communicator, runs the
+ *            one-workgroup form; COCOA_GRAM_MIRROR=0 forces it);
  *   DENSE -- dense rows (cocoa_set_train_dense, d even, d <= 4096): w and
  *            deltaW in registers across a 512-thread workgroup, rows streamed;
  *   AUTO  -- DENSE on dense rows that fit it, else GRAM on sparse rows (mean
