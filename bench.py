@@ -488,8 +488,12 @@ def main():
             tk = json.load(open(tf)).get("kernels", {})
             rec = tk.get("solver_" + plan.get("solver", ""))
             traffic = rec["hbm_bytes_per_launch"] if rec else None
+            # the evaluation's passes: the cold pass (eval_stream_kernel) and, with the
+            # hot / cold split, the hot pass before it
             rec = tk.get("eval")
             traffic_eval = rec["hbm_bytes_per_launch"] if rec else None
+            if traffic_eval is not None and plan.get("eval_split") and tk.get("eval_hot"):
+                traffic_eval += tk["eval_hot"]["hbm_bytes_per_launch"]
         except Exception:
             traffic = traffic_eval = None
     # the eval's launch average over the timed region (HIP events on the

@@ -3659,7 +3659,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
                   "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d,"
-                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld,\"mbsgd_pull\":%d}",
+                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld,\"mbsgd_pull\":%d,\"eval_split\":%d}",
                   ctx->use_gram ? ctx->gram_chunks : 0, ctx->gram_mirror && !ctx->device_shared() ? 1 : 0,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
@@ -3668,7 +3668,8 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   ctx->dw_compact ? 1 : 0, (long long)ctx->max_u, (long long)ctx->sum_u,
                   !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
                   ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot, ctx->dw_priv ? 1 : 0,
-                  (long long)ctx->max_uh, (long long)ctx->n_tail, ctx->mbsgd_pull ? 1 : 0);
+                  (long long)ctx->max_uh, (long long)ctx->n_tail, ctx->mbsgd_pull ? 1 : 0,
+                  ctx->split_ready && !ctx->strict ? 1 : 0);
     require(wrote >= 0 && wrote < len, COCOA_E_ARG, "cocoa_plan_info: buffer too small");
     CAPI_END(ctx)
 }

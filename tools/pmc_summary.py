@@ -51,7 +51,8 @@ def main():
     tags = (("solver_chain", "solver_kernel<", ()), ("solver_gram", "solver_gram_kernel", ()),
             ("solver_dense", "dense_solver_kernel", ()), ("gram", "gram_kernel", ("solver_gram",)),
             ("gram_seq", "gram_seq_kernel", ()), ("gram_list", "gram_list_kernel", ()),
-            ("eval", "eval_stream_kernel", ()), ("eval_dense", "eval_dense_kernel", ()),
+            ("eval", "eval_stream_kernel", ()), ("eval_hot", "eval_hot_kernel", ()),
+            ("eval_dense", "eval_dense_kernel", ()),
             ("plan", "plan_kernel", ()), ("fold", "fold_kernel", ("compact",)),
             ("fold_compact", "fold_compact_kernel", ()), ("fold_blocks", "fold_blocks_kernel", ()),
             ("apply", "apply_kernel", ()))
