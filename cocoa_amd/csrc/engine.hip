@@ -626,7 +626,7 @@ static void upload_padded(DevBuf& b, const void* src, size_t bytes, hipStream_t 
 // Row tiles for the fast eval pass: whole rows, <= kEvalTile entries and rows
 // per tile; a row longer than kEvalTile is a tile of its own.
 static int64_t make_tiles(const int64_t* row_ptr, int64_t n, DevBuf& out, hipStream_t s, int64_t cap = kEvalTile,
-                          int64_t row_cap = -1) {
+                          int64_t row_cap = kEvalRows) {
     if (row_cap < 0) row_cap = cap;
     std::vector<int64_t> t{0};
     int64_t r = 0;

@@ -48,7 +48,8 @@ constexpr int kRegChunks = COCOA_REG_CHUNKS;  // rows with z <= 64 * kRegChunks 
 constexpr int short_row_chunks(int mode, bool strict) {
     return (strict || mode == 1) ? kRegChunks : (mode == 2 ? (kRegChunks < 2 ? kRegChunks : 2) : (kRegChunks < 3 ? kRegChunks : 3));
 }
-constexpr int kEvalTile = 4096;     // entries (and max rows) per fast-eval tile
+constexpr int kEvalTile = 4096;     // entries per fast-eval tile
+constexpr int kEvalRows = 512;      // rows per fast-eval tile (their y / row_base staged in LDS up front)
 
 // Per-batch step metadata, staged by the loader wave in LDS (SoA).
 struct BatchMeta {

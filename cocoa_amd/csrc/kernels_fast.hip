@@ -288,6 +288,11 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
     __shared__ uint16_t roff[TILE + 2];
     __shared__ double red[BLOCK / 64];
     __shared__ double whot[HOT > 0 ? HOT : 1];
+    // the tile's labels (and hot-pass dots) loaded with its row offsets, up front:
+    // read per row after its LDS sum, each was a dependent global round trip per
+    // row a 16-lane group takes (C2's cold pass: ~8 rows per group and tile)
+    __shared__ double yl[kEvalRows];
+    __shared__ double bl[BASE ? kEvalRows : 1];
     const int tid = threadIdx.x;
     if (HOT > 0) {
         const int32_t h = (int32_t)min<int64_t>(HOT, a.d);
@@ -325,7 +330,13 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             continue;
         }
         const int nr = (int)(r1 - r0);
-        for (int i = tid; i <= nr; i += BLOCK) roff[i] = (uint16_t)(rp[r0 + i] - e0);
+        for (int i = tid; i <= nr; i += BLOCK) {
+            roff[i] = (uint16_t)(rp[r0 + i] - e0);
+            if (i < nr) {
+                yl[i] = yy[r0 + i];
+                if (BASE && !test) bl[i] = a.row_base[r0 + i];
+            }
+        }
         const int64_t base = e0 & ~(int64_t)3;
         const int sh = (int)(e0 - base);  // prod[k] holds entry base + k; rows index from sh
         const int64_t span = e1 - base;
@@ -362,11 +373,11 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             double dot = row16_sum(acc);
             if (sub == 0) {
                 if (!test) {
-                    if (BASE) dot += a.row_base[r0 + r];
-                    hinge += jmax(1 - yy[r0 + r] * dot, 0.0);
+                    if (BASE) dot += bl[r];
+                    hinge += jmax(1 - yl[r] * dot, 0.0);
                     if (a.row_xw) a.row_xw[r0 + r] = dot;
                 } else {
-                    err += (dot * yy[r0 + r] > 0) ? 0.0 : 1.0;
+                    err += (dot * yl[r] > 0) ? 0.0 : 1.0;
                 }
             }
         }
@@ -678,16 +689,36 @@ void eval_split_tiles(int* hot_cap, int* cold_cap) {
     *cold_cap = COCOA_COLD_TILE;
 }
 
+// A grid-stride pass with more blocks than fit the device at once runs its
+// last ones as a second wave over the same number of tiles each: cap the grid at
+// the kernel's resident blocks (its LDS sets how many share a CU).
+template <typename F>
+static int resident_grid(F kernel, int threads, int want) {
+    int per_cu = 0, dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1) {
+        (void)hipGetLastError();
+        return want;
+    }
+    return std::max(1, std::min(want, per_cu * cus));
+}
+
 // the split evaluation: hot pass, then the cold pass over a's (cold) train CSR
 // and the (unsplit) test rows
 static bool launch_eval_split(const EvalArgs& a, int blocks, hipStream_t s) {
     const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
     const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_h_tiles, 256 * COCOA_HOT_WGS));
     eval_hot_kernel<COCOA_HOT_TILE, COCOA_HOT_BLOCK, kEvalHot><<<hb, COCOA_HOT_BLOCK, 0, s>>>(a);
-    if (c16)
+    if (c16) {
+        blocks = resident_grid(eval_stream_kernel<COCOA_COLD_TILE, COCOA_COLD_BLOCK, true, 0, 0, true>, COCOA_COLD_BLOCK,
+                               blocks);
         eval_stream_kernel<COCOA_COLD_TILE, COCOA_COLD_BLOCK, true, 0, 0, true><<<blocks, COCOA_COLD_BLOCK, 0, s>>>(a);
-    else
+    } else {
+        blocks = resident_grid(eval_stream_kernel<COCOA_COLD_TILE, COCOA_COLD_BLOCK, false, 0, 0, true>,
+                               COCOA_COLD_BLOCK, blocks);
         eval_stream_kernel<COCOA_COLD_TILE, COCOA_COLD_BLOCK, false, 0, 0, true><<<blocks, COCOA_COLD_BLOCK, 0, s>>>(a);
+    }
     if (!a.counter) eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
     return a.counter && a.out_host;
 }
@@ -700,12 +731,16 @@ bool launch_eval_fast(const EvalArgs& a, int blocks, hipStream_t s) {
     u.counter = nullptr;  // the variants end with eval_final_kernel
     if (launch_eval_diag(u, c16, s)) return false;
 #endif
-    if (c16)
+    if (c16) {
+        blocks = resident_grid(eval_stream_kernel<kEvalTile, 512, true>, 512, blocks);
         eval_stream_kernel<kEvalTile, 512, true><<<blocks, 512, 0, s>>>(a);
-    else if (a.d > kEvalWideD)
+    } else if (a.d > kEvalWideD) {
+        blocks = resident_grid(eval_stream_kernel<2048, 512, false, 0, 4096>, 512, blocks);
         eval_stream_kernel<2048, 512, false, 0, 4096><<<blocks, 512, 0, s>>>(a);
-    else
+    } else {
+        blocks = resident_grid(eval_stream_kernel<kEvalTile, 512, false>, 512, blocks);
         eval_stream_kernel<kEvalTile, 512, false><<<blocks, 512, 0, s>>>(a);
+    }
     if (!a.counter) eval_final_kernel<<<1, 256, 0, s>>>(a.partials, blocks, a.out);
     return a.counter && a.out_host;
 }

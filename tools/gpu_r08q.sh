@@ -1,0 +1,12 @@
+#!/bin/bash
+# eval with the tile's labels / hot dots staged up front: eval tests, then C2 / C4 A/B
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+O=gpurun_out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_eval_split.py tests/test_gpu_parity.py tests/test_gpu_configs.py -k "eval or c2 or c4 or parity" -m gpu -x -v --timeout 300 \
+  --timeout-method thread > $O/gpu_tests_r08q.log 2>&1; rc=$?
+grep -E "passed|failed|error" $O/gpu_tests_r08q.log | tail -3; [ $rc -eq 0 ] || exit $rc
+STEPS=50 REPS=2 TAG=ab8q tools/benchab.sh " --" "COCOA_EVAL_SPLIT=0 --" || exit $?
+STEPS=10 REPS=1 TAG=ab8qc4 tools/benchab.sh "-- --config c4" "COCOA_EVAL_SPLIT=0 -- --config c4" || exit $?
+TAG=r08q tools/gpu_run.sh prof || exit $?
