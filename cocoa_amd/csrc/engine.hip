@@ -173,7 +173,7 @@ struct cocoa_ctx {
     int32_t K_loc = 0, K_glob = 0, part_begin = 0, d = 0;
     Csr tr;
     DevBuf sqn, rowflags, part_ptr;
-    DevBuf row_zc;  // fast mode: per row, ends of the column-class runs (4 int32), see set_train_impl
+    DevBuf row_zc;  // fast mode: per row, ends of the column runs (kGramRuns int32), see set_train_impl
     std::vector<int64_t> h_part_ptr;
     bool any_dup = false;
     bool tr_dense = false;  // every row stores columns 0..d-1 in order (val = X[n][d])
@@ -283,7 +283,7 @@ struct cocoa_ctx {
     // may be attached after cocoa_init).
     bool shared_dev = false;   // (cocoa_create_multi: another member has this ordinal)
     bool device_shared() const;
-    int32_t hot_split = 0;     // hot / cold run boundary of the fast-mode rows (COCOA_HOTRUNS)
+    int32_t hot_split = 0;     // (unused: 0)
     DevBuf xbase;              //   their partial-base exchange ([K][4][kXbR][16][2] tagged granules)
     int32_t xtag_epoch = 0;    //   launch counter in the granule tags
     hipStream_t gstream = nullptr;
@@ -1038,19 +1038,34 @@ static void build_eval_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::
     std::vector<uint16_t> hc((size_t)std::max<int64_t>(nh, 1));
     std::vector<double> hv((size_t)std::max<int64_t>(nh, 1)), cv((size_t)std::max<int64_t>(nc, 1));
     std::vector<int32_t> cc((size_t)std::max<int64_t>(nc, 1));
-    for (int64_t r = 0; r < n; ++r) {
-        int64_t a = hp[(size_t)r], b = cp[(size_t)r];
-        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) {
-            const int32_t c = pcol[(size_t)q];
-            if (c < kEvalHot) {
-                hc[(size_t)a] = (uint16_t)c;
-                hv[(size_t)a++] = val[q];
-            } else {
-                cc[(size_t)b] = c;
-                cv[(size_t)b++] = val[q];
+    // each part of a row in ascending device column: neighbouring lanes of a gather
+    // then read neighbouring words of w (fewer lines per gather instruction, fewer
+    // LDS bank conflicts in the hot pass); the sums are reassociated anyway
+    const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int tix = 0; tix < T; ++tix)
+        th.emplace_back([&, tix] {
+            std::vector<std::pair<int32_t, double>> tmp;
+            for (int64_t r = n * tix / T; r < n * (tix + 1) / T; ++r) {
+                tmp.clear();
+                for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) tmp.emplace_back(pcol[(size_t)q], val[q]);
+                std::stable_sort(tmp.begin(), tmp.end(),
+                                 [](const std::pair<int32_t, double>& x, const std::pair<int32_t, double>& y) {
+                                     return x.first < y.first;
+                                 });
+                int64_t a = hp[(size_t)r], b = cp[(size_t)r];
+                for (const auto& cvp : tmp) {
+                    if (cvp.first < kEvalHot) {
+                        hc[(size_t)a] = (uint16_t)cvp.first;
+                        hv[(size_t)a++] = cvp.second;
+                    } else {
+                        cc[(size_t)b] = cvp.first;
+                        cv[(size_t)b++] = cvp.second;
+                    }
+                }
             }
-        }
-    }
+        });
+    for (auto& t : th) t.join();
     ctx->hot_tr.n = ctx->cold_tr.n = n;
     ctx->hot_tr.nnz = nh;
     ctx->cold_tr.nnz = nc;
@@ -1164,7 +1179,7 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
         pcol.resize((size_t)std::max<int64_t>(nnz, 1));
         for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];
     }
-    // Fast mode: every row stores its entries in four runs (device column
+    // Fast mode: every row stores its entries in kGramRuns runs (device column
     // c % kGramRuns), each in stored order, so that each of
     // the Gram solver's memory waves (solver_gram.h) streams one contiguous run
     // per row.  Only the fast kernels see this order (their dots are
@@ -1175,19 +1190,12 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     // (device column parity splits the entries evenly; a hot / cold split -- the
     // LDS-resident columns vs the rest, or the columns holding the first half of
     // the entries vs the rest -- measured 3.93 / 2.97 ms against 2.70: the first
-    // class's fetch and memory waves carry most of the units; r03 A/B)
-    // (COCOA_HOTRUNS: parity, then the LDS-resident columns of the Gram solver
-    // [0, hot_split) before the rest; COCOA_HOT_SPLIT=j moves the boundary down)
-    int32_t hsplit = -1;
-    if (COCOA_HOTRUNS) {
-        gram_solver_lds(num_features, &hsplit);
-        if (const char* e = std::getenv("COCOA_HOT_SPLIT")) hsplit = std::max(0, std::min(hsplit, std::atoi(e)));
-    }
-    ctx->hot_split = std::max(hsplit, 0);
-    auto class_of = [&](int32_t c) -> int { return hsplit >= 0 ? 2 * (c & 1) + (c >= hsplit ? 1 : 0) : c % kGramRuns; };
+    // class's fetch and memory waves carry most of the units; r03 A/B; the
+    // mirrored halves' hot / cold runs 2.85 against 2.67 ms, r06p)
+    ctx->hot_split = 0;
     if (split_classes) {
         pval.resize((size_t)nnz);
-        zcv.resize((size_t)std::max<int64_t>(n_rows, 1) * 4);
+        zcv.resize((size_t)std::max<int64_t>(n_rows, 1) * kGramRuns);
         std::vector<int32_t> ncol((size_t)std::max<int64_t>(nnz, 1));
         const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         std::vector<std::thread> th;
@@ -1196,16 +1204,16 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
                 for (int64_t r = n_rows * tix / T; r < n_rows * (tix + 1) / T; ++r) {
                     const int64_t b = row_ptr[r], e = row_ptr[r + 1];
                     int64_t cnt[kGramRuns] = {}, at[kGramRuns];
-                    for (int64_t q = b; q < e; ++q) ++cnt[class_of(pcol[(size_t)q])];
+                    for (int64_t q = b; q < e; ++q) ++cnt[pcol[(size_t)q] % kGramRuns];
                     int64_t run = b;
                     for (int c = 0; c < kGramRuns; ++c) {
                         at[c] = run;
                         run += cnt[c];
                     }
-                    for (int c = 0; c < 4; ++c)  // ends of runs 0..2 (row-relative), then the row length
-                        zcv[(size_t)r * 4 + c] = (int32_t)((c < kGramRuns - 1 ? at[c] + cnt[c] : e) - b);
+                    for (int c = 0; c < kGramRuns; ++c)  // ends of runs 0 .. R-2 (row-relative), then the row length
+                        zcv[(size_t)r * kGramRuns + c] = (int32_t)((c < kGramRuns - 1 ? at[c] + cnt[c] : e) - b);
                     for (int64_t q = b; q < e; ++q) {
-                        const int64_t dst = at[class_of(pcol[(size_t)q])]++;
+                        const int64_t dst = at[pcol[(size_t)q] % kGramRuns]++;
                         ncol[(size_t)dst] = pcol[(size_t)q];
                         pval[(size_t)dst] = val[q];
                     }
@@ -1228,7 +1236,7 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     }
     upload_padded(ctx->tr.val, split_classes ? pval.data() : val, sizeof(double) * (size_t)nnz, s);
     if (split_classes)
-        upload(ctx->row_zc, zcv.data(), sizeof(int32_t) * 4 * (size_t)n_rows, s);
+        upload(ctx->row_zc, zcv.data(), sizeof(int32_t) * kGramRuns * (size_t)n_rows, s);
     else
         ctx->row_zc.free();
     upload(ctx->tr.y, y, sizeof(double) * (size_t)n_rows, s);
@@ -1729,7 +1737,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
         ctx->plan_beg.alloc(steps * sizeof(int64_t));
         ctx->plan_z.alloc(steps * sizeof(int32_t));
         if (ctx->row_zc.p || ctx->use_gram)  // (the Gram solver's loader reads the step's look-back there)
-            ctx->plan_zc.alloc(steps * 4 * sizeof(int32_t));
+            ctx->plan_zc.alloc(steps * kGramRuns * sizeof(int32_t));
         else
             ctx->plan_zc.free();
         ctx->plan_y.alloc(steps * sizeof(double));
@@ -1741,7 +1749,7 @@ extern "C" int cocoa_init(cocoa_ctx* ctx, const cocoa_params* params, const coco
             ctx->plan_beg2.alloc(steps * sizeof(int64_t));
             ctx->plan_z2.alloc(steps * sizeof(int32_t));
             if (ctx->row_zc.p || ctx->use_gram)
-                ctx->plan_zc2.alloc(steps * 4 * sizeof(int32_t));
+                ctx->plan_zc2.alloc(steps * kGramRuns * sizeof(int32_t));
             else
                 ctx->plan_zc2.free();
             ctx->plan_y2.alloc(steps * sizeof(double));

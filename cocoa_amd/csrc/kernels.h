@@ -14,30 +14,29 @@ namespace cocoa {
 enum SolverMode : int { MODE_PLUS = 0, MODE_COCOA = 1, MODE_MBCD = 2, MODE_LSGD = 3 };
 
 constexpr int kWave = 64;
-// deltaW column classes of the Gram solver (solver_gram.h).  In fast mode every
-// row stores its entries in four runs by device column c % kGramRuns
-// (cocoa_set_train), with the ends of runs 0 .. 2 per row in row_zc (4 int32 a
-// row: three ends and the row length).  A solver workgroup has kGramClasses
-// memory / fetch waves: class lc of the one-workgroup solver takes runs 2 lc and
-// 2 lc + 1 (c % 4 in {2 lc, 2 lc + 1}); the mirrored solver's half h (two
-// workgroups per partition) takes run 2 lc + h, so half h owns the columns of
-// parity h.
-#ifndef COCOA_GNC
-#define COCOA_GNC 2
+// deltaW column runs of the Gram solver (solver_gram.h).  In fast mode every
+// row stores its entries in kGramRuns runs by device column c % kGramRuns
+// (cocoa_set_train), with the ends of runs 0 .. kGramRuns-2 and the row length
+// per row in row_zc (kGramRuns int32 a row).  A solver workgroup has one memory
+// wave and one fetch wave per column class: the one-workgroup solver has 2
+// classes, class lc taking the runs [lc R/2, (lc + 1) R/2); the mirrored
+// solver's half h (two workgroups per partition) has R/2 classes, class lc
+// taking run 2 lc + h, so half h owns the columns of parity h.
+// COCOA_RUNS=8 (round 6, measured and not the default): each mirrored half then
+// has four memory waves, each with half the units per batch.  A diag build
+// with half the units per memory wave had shown the solver 2.03 -> 1.60 ms;
+// with eight runs, the loader's per-class work vectorised and the counters read
+// at once, the C2 solver measured 1.727-1.729 against 1.745-1.752 ms for four
+// runs on one box, but the step did not move (2.008-2.010 against 1.998-2.005
+// ms): the next round's Gram rows, 1.61 ms beside the solver, then still run
+// into the evaluation.
+#ifndef COCOA_RUNS
+#define COCOA_RUNS 4
 #endif
-constexpr int kGramClasses = COCOA_GNC;
-static_assert(kGramClasses == 2, "column classes per workgroup");
-constexpr int kGramRuns = 4;        // column runs of a fast-mode row
-// COCOA_HOTRUNS=1: run = 2 (c & 1) + (c >= hot_split) -- even hot, even cold, odd
-// hot, odd cold -- so a class (one per parity) is its hot run then its cold run,
-// and the mirrored solver's half h gives its two memory waves the hot and the
-// cold run of parity h (LDS-only and global-only code).  0: run = c % 4.
-// (r06p, one box: the hot / cold classes 2.85 ms against 2.67 for c % 4 -- the
-// hot-only wave carries ~70% of the half's entries; COCOA_HOT_SPLIT lowers it)
-#ifndef COCOA_HOTRUNS
-#define COCOA_HOTRUNS 0
-#endif
-constexpr int kProfStride = 64;     // solver profile words per partition (diagnostics)
+constexpr int kGramRuns = COCOA_RUNS;  // column runs of a fast-mode row
+static_assert(kGramRuns == 4 || kGramRuns == 8, "column runs");
+constexpr int kGramClasses = 2;        // classes of the one-workgroup solver
+constexpr int kProfStride = 128;    // solver profile words per partition (diagnostics)
 constexpr int kMetaSteps = 64;      // steps per staged batch (one per loader lane)
 #ifndef COCOA_REG_CHUNKS
 #define COCOA_REG_CHUNKS 4
@@ -134,12 +133,12 @@ struct PlanArgs {
     int32_t H;
     int32_t need_xw;
     const double* xw_cache;   // per-row x.w of the current w from the last fast eval, or null
-    const int32_t* row_zc;    // per row: 4 int32, ends of the class runs 0 .. kGramClasses-2 (fast mode), or null
+    const int32_t* row_zc;    // per row: kGramRuns int32, ends of runs 0 .. kGramRuns-2 and the row length (fast mode), or null
     const int32_t* row_zs;    // private columns: per row its shared entries (the step's z), or null
     int64_t* beg;
     int32_t* z;
-    int32_t* zc;              // per step: 4 int32, the ends of its row's runs 0..2 (row_zc, or all z) and its
-                              // look-back (plan_impl.h), or null
+    int32_t* zc;              // per step: kGramRuns int32, the ends of its row's runs 0 .. kGramRuns-2 (row_zc, or
+                              // all z) and its look-back (plan_impl.h), or null
     int32_t win;              // the Gram solver's window (steps) for the look-back; 0: none
     double* py;
     double* pq;
@@ -173,7 +172,7 @@ struct GramSolverArgs {
     const int32_t* samples;
     const int64_t* plan_beg;
     const int32_t* plan_z;
-    const int32_t* plan_zc;   // per step: 4 int32, ends of the rows' runs 0..2 and the step's look-back (PlanArgs)
+    const int32_t* plan_zc;   // per step: kGramRuns int32, ends of the rows' runs and the step's look-back (PlanArgs)
     const double* plan_y;
     const double* plan_q;
     const double* plan_xw;
@@ -329,7 +328,7 @@ int eval_tile_entries(int64_t d);
 void launch_plan_fast(const PlanArgs& a, hipStream_t s);
 // Gram-window solver: lds bytes for a partition of max_nl rows (alpha in LDS
 // when it fits, else in alpha_work)
-size_t gram_solver_lds(int64_t d, int32_t* hot);
+size_t gram_solver_lds(int64_t d, int32_t* hot, bool mirror = false);
 void launch_gram(const GramArgs& a, hipStream_t s);
 size_t gram_seq_lds();  // LDS bytes of gram_seq_kernel (one workgroup per CU)
 int gram_window_batches();  // batches in the Gram solver's look-back window (kGNB)

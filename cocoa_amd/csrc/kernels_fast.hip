@@ -21,9 +21,10 @@ void launch_solver_fast(int mode, bool vec_lds, bool alpha_lds, const SolverArgs
 void launch_plan_fast(const PlanArgs& a, hipStream_t s) { launch_plan_impl<false>(a, s); }
 
 // ------------------------------------------------- Gram-window solver --
-size_t gram_solver_lds(int64_t d, int32_t* hot) {
+size_t gram_solver_lds(int64_t d, int32_t* hot, bool mirror) {
     constexpr size_t kLds = 160 * 1024;
-    const size_t base = (sizeof(GramSolverLds) + 15) & ~(size_t)15;
+    const size_t st = mirror ? sizeof(GramSolverLdsT<kGramRuns / 2>) : sizeof(GramSolverLdsT<kGramClasses>);
+    const size_t base = (st + 15) & ~(size_t)15;
     // the most frequent columns (device order) of deltaW in the remaining LDS
     const int64_t h = std::max<int64_t>(0, std::min<int64_t>(d, (int64_t)((kLds - base) / sizeof(double)) & ~(int64_t)63));
     if (hot) *hot = (int32_t)h;
@@ -108,12 +109,13 @@ static void launch_sg4(const GramSolverArgs& a, int grid, size_t lds, hipStream_
     if (MIR_OK && a.mirror) {
         (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XWM, MIR_OK>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        solver_gram_kernel<MODE, HOTLDS, PROJ, XWM, MIR_OK><<<2 * grid, kGThreads + 64, lds, s>>>(a);
+        solver_gram_kernel<MODE, HOTLDS, PROJ, XWM, MIR_OK>
+            <<<2 * grid, GCfg<kGramRuns / 2>::kThreads + 64, lds, s>>>(a);
         return;
     }
     (void)hipFuncSetAttribute((const void*)solver_gram_kernel<MODE, HOTLDS, PROJ, XWM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    solver_gram_kernel<MODE, HOTLDS, PROJ, XWM><<<grid, kGThreads, lds, s>>>(a);
+    solver_gram_kernel<MODE, HOTLDS, PROJ, XWM><<<grid, GCfg<kGramClasses>::kThreads, lds, s>>>(a);
 }
 // the loader's x.w: xw_produce_kernel's flags or the plan's (MbCD has no Gram
 // rows, hence no side stream and no producer: always the plan's).  Measured and
@@ -166,7 +168,7 @@ static bool gram_hot_lds() {
 
 void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t s) {
     GramSolverArgs g = a;
-    size_t lds = gram_solver_lds(a.d, &g.hot);
+    size_t lds = gram_solver_lds(a.d, &g.hot, a.mirror != 0);
 #ifdef COCOA_DIAG
     // diagnostic builds only (make diag): timing experiments, results invalid with DIAG
     if (const char* e = getenv("COCOA_GRAM_HOT")) {  // cap the LDS-resident columns
@@ -176,12 +178,11 @@ void launch_solver_gram(int mode, const GramSolverArgs& a, int grid, hipStream_t
     }
     if (const char* e = getenv("COCOA_GRAM_DIAG")) g.diag = atoi(e);
 #endif
-    if (g.hot_split > g.hot) g.hot_split = 0;  // (a hot-only class must be LDS-resident)
+    g.hot_split = 0;
     if (!gram_hot_lds() || g.hot == 0) {
-        lds -= sizeof(double) * (size_t)g.hot;
-        g.hot = 0;
         g.mirror = 0;  // (the mirrored form keeps the hot columns in LDS)
-        g.hot_split = 0;
+        lds = (sizeof(GramSolverLdsT<kGramClasses>) + 15) & ~(size_t)15;
+        g.hot = 0;
         if (mode == MODE_PLUS) launch_sg<MODE_PLUS, false>(g, grid, lds, s);
         else if (mode == MODE_COCOA) launch_sg<MODE_COCOA, false>(g, grid, lds, s);
         else if (mode == MODE_LSGD) launch_sg3<MODE_LSGD, false, false>(g, grid, lds, s);

@@ -68,11 +68,16 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
         __builtin_nontemporal_store(a.sqn[gr], a.pq + g);
         if (a.xw) __builtin_nontemporal_store(xw, a.xw + g);  // (null: xw_produce_kernel forms x.w)
         if (a.zc) {
-            // the ends of the row's column runs 0..2 (all of it in run 0 without row_zc),
-            // and the step's look-back (above) in the fourth word
+            // the ends of the row's column runs 0 .. R-2 (all of it in run 0 without
+            // row_zc), and the step's look-back (above) in the last word (the row's
+            // length there is plan z's)
             typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
             const int32_t zz = (int32_t)(e - b);
-            i32x4 z4 = a.row_zc ? *(const i32x4*)(a.row_zc + 4 * gr) : i32x4{zz, zz, zz, zz};
+            if (kGramRuns == 8) {
+                const i32x4 lo = a.row_zc ? *(const i32x4*)(a.row_zc + kGramRuns * gr) : i32x4{zz, zz, zz, zz};
+                __builtin_nontemporal_store(lo, (i32x4*)(a.zc + kGramRuns * g));
+            }
+            i32x4 z4 = a.row_zc ? *(const i32x4*)(a.row_zc + kGramRuns * gr + kGramRuns - 4) : i32x4{zz, zz, zz, zz};
             int32_t prev = -1;
             if (a.win > 0) {
                 const int32_t j = (int32_t)(g - (int64_t)k * a.H);
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(256) void plan_kernel(PlanArgs a) {
                     }
             }
             z4.w = prev;
-            __builtin_nontemporal_store(z4, (i32x4*)(a.zc + 4 * g));
+            __builtin_nontemporal_store(z4, (i32x4*)(a.zc + kGramRuns * g + kGramRuns - 4));
         }
     }
 }

@@ -126,6 +126,14 @@ __device__ __forceinline__ bool wait_ge(const int* p, int v, int* abort_flag, in
         __builtin_amdgcn_s_sleep(1);
     }
 }
+// n counters at once: one LDS round trip and one fence when all are >= v already
+// (the common case), else wait_ge on each
+__device__ __forceinline__ bool all_ge_now(const int* p, int n, int v) {
+    bool ok = true;
+    for (int i = 0; i < n; ++i) ok = ok && __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    return ok;
+}
 // L1-bypassing read of the deltaW slice (the scatter wave's atomics land in L2)
 __device__ __forceinline__ double dw_load(const double* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -819,13 +827,8 @@ __global__ __launch_bounds__(kGsThreads, 1) void gram_seq_kernel(GramArgs a) {
 // issue-bound part of the round -- run side by side.  The chain adds the
 // partial bases.
 constexpr int kGWin = kGW + kGB;         // loader's look-back for alpha forwarding: the window + 1 batch
-constexpr int kGNC = kGramClasses;       // column classes = memory waves = fetch waves
-constexpr int kGE = 8192;                // staged entries (LDS ring positions), all classes
-constexpr int kGSub = kGE / 64 / kGNC;   // 64-entry units of one class's sub-ring
 constexpr int kGUnitB = 64 * 13;         // bytes of one 64-entry ring unit
 constexpr int kGOCol = 0, kGOLo = 256, kGOHi = 512, kGORow = 768;  // its fields
-constexpr int kGMaxU = kGSub / 4;        // units of one class of a staged batch (4 live batches per
-                                         // sub-ring); larger batches go direct
 constexpr int kGGt = 4;                  // Gram-row ring (batches)
 #ifndef COCOA_EARLY_RELEASE
 #define COCOA_EARLY_RELEASE 0  // 1: memory waves free a staged batch's slots before its atomics (r06n: solver 2.34 -> 2.39 ms, not kept)
@@ -834,19 +837,44 @@ constexpr int kGGt = 4;                  // Gram-row ring (batches)
 #define COCOA_GPART 16  // (32: 1.4% slower, 544 fewer LDS-resident deltaW columns; r03 A/B)
 #endif
 constexpr int kGPart = COCOA_GPART;      // product slots per row (lanes l, l + kGPart, ... share one)
+// Shape of a workgroup with NC column classes (one memory wave and one fetch
+// wave each): the one-workgroup solver has 2, the mirrored solver's halves
+// kGramRuns / 2.  Staged entries: an LDS ring of kE positions, a sub-ring of
+// kSub 64-entry units per class holding 4 live batches of up to kMaxU units
+// (larger batches go direct).  With four classes the ring is halved (4,096
+// positions, 4 units = 256 entries of a class per batch: 98.6% of C2's
+// (batch, run) pairs with eight runs) so that the hot image keeps its LDS.
 // Wave roles.  Wave w of the workgroup runs on SIMD w % 4, and which waves
 // share a SIMD matters (r03 A/B on C2, two classes): chain + loader on one
 // SIMD and the two fetch waves on another, 2.97 ms; chain + fetch 0 and
-// loader + fetch 1, 2.85 ms; the memory waves keep a SIMD each.  Four classes
-// (ten waves, a memory wave beside the chain) measured 3.35 ms.
-enum GRole : int { kRChain = 0, kRLoader = 1, kRMem = 2, kRFetch = 2 + kGNC, kRIdle = 2 + 2 * kGNC, kRRelay = 3 + 2 * kGNC };
-#ifndef COCOA_GLAYOUT
-#define COCOA_GLAYOUT kRChain, kRLoader, kRMem, kRMem + 1, kRFetch, kRFetch + 1
-#endif
-constexpr int kGRoles[] = {COCOA_GLAYOUT};
-constexpr int kGWaves = (int)(sizeof(kGRoles) / sizeof(int));
-constexpr int kGThreads = 64 * kGWaves;
-static_assert(kGNC == 2 || kGWaves == 2 + 2 * kGNC, "wave layout");
+// loader + fetch 1, 2.85 ms; the memory waves keep a SIMD each (with four
+// classes, two memory waves share each of SIMDs 2 and 3).  Waves: chain,
+// loader, then groups of (memory, memory, fetch, fetch); the mirrored form adds
+// the relay as the last wave.
+template <int NC>
+struct GCfg {
+    static constexpr int kE = NC == 2 ? 8192 : 4096;
+    static constexpr int kSub = kE / 64 / NC;
+    static constexpr int kMaxU = kSub / 4;
+    static constexpr int kRChain = 0, kRLoader = 1, kRMem = 2, kRFetch = 2 + NC, kRIdle = 2 + 2 * NC,
+                         kRRelay = 3 + 2 * NC;
+    static constexpr int kWaves = 2 + 2 * NC;
+    static constexpr int kThreads = 64 * kWaves;
+    // counters (LDS, release / acquire); kCScat .. kCFetch: one per class; kCBase
+    // + r: the partial base of column run r (kGramRuns of them: the one-workgroup
+    // solver uses r < NC, one per class; the mirrored one every run)
+    static constexpr int kCScat = 3, kCBase = kCScat + NC, kCFreed = kCBase + kGramRuns, kCFetch = kCFreed + NC;
+    static_assert(kCFetch + NC <= 32, "counters");
+    static_assert(NC == 2 || NC == 4, "classes");
+    __device__ static int role(int w) {
+        if (w == 0) return kRChain;
+        if (w == 1) return kRLoader;
+        if (w >= kWaves) return kRIdle;
+        const int i = w - 2, g = i >> 2, j = i & 3;
+        return j < 2 ? kRMem + 2 * g + j : kRFetch + 2 * g + (j - 2);
+    }
+};
+constexpr int kCChain = 0, kCLoad = 1, kCAbort = 2;
 
 struct GRec {                          // one step (64 B)
     double B, Y, AE, YA;               // AE, YA: set by the chain (its alpha prefetch or a forward)
@@ -867,32 +895,26 @@ struct GLay {                          // one batch's rows of one class, for the
     int32_t T;                         // entries
 };
 
-// counters (LDS, release / acquire); kCScat .. kCFetch: one per class
-// kCBase + r: the partial base of column run r (kGramRuns of them: the
-// one-workgroup solver uses r < kGNC, one per class; the mirrored one all four)
-constexpr int kCChain = 0, kCLoad = 1, kCAbort = 2, kCScat = 3, kCBase = kCScat + kGNC, kCFreed = kCBase + kGramRuns,
-              kCFetch = kCFreed + kGNC;
-static_assert(kCFetch + kGNC <= 32, "counters");
-
-struct GramSolverLds {
+template <int NC>
+struct GramSolverLdsT {
     int cnt[32];
     double lsgd_s;                     // MODE_LSGD: s after the last step (loader -> epilogue)
     int32_t lsgd_keep, lsgd_pad;       //   and whether wInit survived (no zero shrink)
     GRec rec[kGRing * kGB];            // ring: (b % kGRing) * kGB + i
     double coef[kGRing * 2 * kGB];     // c_j, same ring (chain -> memory waves); [kGB, 2 kGB) of a slot stay 0
-    GLay lay[kGRing][kGNC];            // same ring (loader -> fetch / memory waves)
+    GLay lay[kGRing][NC];              // same ring (loader -> fetch / memory waves)
     double base[kGramRuns][kGSlots];   // partial base_s per class (mirrored: per run) and slot (memory waves -> chain)
-    double part[kGNC][kGB + 1][kGPart];  // memory wave: row partial sums of a batch's products (+ a sink row)
+    double part[NC][kGB + 1][kGPart];  // memory wave: row partial sums of a batch's products (+ a sink row)
     alignas(16) double gring[kGGt][kGB][kGW];      // Gram rows of batch x at [x % kGGt] (loader DMA -> chain)
     // staged entries (fetch waves -> memory waves), 64 per ring unit: columns, value
     // low words, value high words (the LDS DMA moves 4 bytes a lane), row bytes
     // (0xFF: past the batch's entries).  One address per lane and unit reaches all
     // four (immediate offsets; the two value words in one ds_read2).  Class c owns
-    // units [c kGSub, (c + 1) kGSub).
-    alignas(16) uint8_t ring[kGE / 64][kGUnitB];
+    // units [c kSub, (c + 1) kSub).
+    alignas(16) uint8_t ring[GCfg<NC>::kE / 64][kGUnitB];
 };
-
-static_assert(sizeof(GramSolverLds) <= 160 * 1024, "solver_gram_kernel LDS");
+static_assert(sizeof(GramSolverLdsT<2>) <= 160 * 1024 && sizeof(GramSolverLdsT<kGramRuns / 2>) <= 160 * 1024,
+              "solver_gram_kernel LDS");
 
 template <int MODE>
 __device__ __forceinline__ void gram_row_consts(const GramSolverArgs& a, double y, double q, double xw, double& B,
@@ -911,9 +933,9 @@ __device__ __forceinline__ void gram_row_consts(const GramSolverArgs& a, double 
     Y = y * a.inv_lam_n;
 }
 
-// the column run of class c of the mirrored solver's half h (kernels.h COCOA_HOTRUNS):
-// half h owns the columns of parity h in both layouts
-__device__ __forceinline__ int gram_mirror_run(int c, int h) { return COCOA_HOTRUNS ? 2 * h + c : 2 * c + h; }
+// the column run of class c of the mirrored solver's half h: half h owns the
+// columns of parity h
+__device__ __forceinline__ int gram_mirror_run(int c, int h) { return 2 * c + h; }
 
 // packed position q of a batch's rows -> row: largest i with excl[i] <= q
 __device__ __forceinline__ int gram_owner(const int32_t* excl, int32_t q) {
@@ -942,11 +964,14 @@ __device__ __forceinline__ uint32_t gram_pad(int32_t u, int32_t nu) {
     return (uint32_t)((nu - 1 - u) >> 31) & 0xFFu;
 }
 // ring unit of class c's sub-ring position pos (a multiple of 64) + 64 u
+template <int NC>
 __device__ __forceinline__ int32_t ring_unit(int c, int32_t pos, int32_t u) {
-    return c * kGSub + (((pos >> 6) + u) & (kGSub - 1));
+    constexpr int kSub = GCfg<NC>::kSub;
+    return c * kSub + (((pos >> 6) + u) & (kSub - 1));
 }
 // lane's entry of a ring unit: (column, value, row byte)
-__device__ __forceinline__ void ring_get(const GramSolverLds& S, int32_t us, int lane, int32_t& col, double& val,
+template <class L>
+__device__ __forceinline__ void ring_get(const L& S, int32_t us, int lane, int32_t& col, double& val,
                                          uint32_t& row) {
     const uint8_t* b = S.ring[us];
     col = *(const int32_t*)(b + kGOCol + 4 * lane);
@@ -979,12 +1004,22 @@ __device__ __forceinline__ double gram_rule(double u, double aa) {
 // seventh wave (relay) copies the other half's partial bases of every batch
 // from xbase into LDS.  Each half thus scatters and gathers half the entries.
 template <int MODE, bool HOTLDS, bool PROJ, int XWM, bool MIRROR = false>
-__global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolverArgs a) {
+__global__ __launch_bounds__(GCfg<MIRROR ? kGramRuns / 2 : kGramClasses>::kThreads + (MIRROR ? 64 : 0), 1)
+void solver_gram_kernel(GramSolverArgs a) {
     constexpr bool XW = XWM == kXwProducer;  // x.w: plan_xw (kXwPlan) or the producer's flags
+    // column classes: 2, or (mirrored) one per run of the half's parity
+    constexpr int NC = MIRROR ? kGramRuns / 2 : kGramClasses;
+    using C = GCfg<NC>;
+    constexpr int kGSub = C::kSub, kGMaxU = C::kMaxU, kGNC = NC;
+    constexpr int kRLoader = C::kRLoader, kRMem = C::kRMem, kRFetch = C::kRFetch, kRIdle = C::kRIdle,
+                  kRRelay = C::kRRelay, kRChain = C::kRChain;
+    constexpr int kCScat = C::kCScat, kCBase = C::kCBase, kCFreed = C::kCFreed, kCFetch = C::kCFetch;
+    constexpr int kGWaves = C::kWaves, kGThreads = C::kThreads;
+    using Lds = GramSolverLdsT<NC>;
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-    GramSolverLds& S = *(GramSolverLds*)lds_raw;
+    Lds& S = *(Lds*)lds_raw;
     // LDS after the hand-off state: deltaW of the hot columns, a.hot doubles
-    double* hotl = (double*)(lds_raw + ((sizeof(GramSolverLds) + 15) & ~(size_t)15));
+    double* hotl = (double*)(lds_raw + ((sizeof(Lds) + 15) & ~(size_t)15));
     const int32_t hot = HOTLDS ? a.hot : 0;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int KP = MIRROR ? (int)(gridDim.x / 2) : (int)gridDim.x;
@@ -1007,19 +1042,16 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         }
     }
     // hot columns [0, hotc), column c at hotl[hix(c)].  A mirrored half only
-    // touches the columns of its parity (runs h, 2 + h), so its image holds those
+    // touches the columns of its parity (its runs 2 c + h), so its image holds those
     // alone: twice the hot columns in the same LDS (C2: 1,472 -> 2,944, 68% -> 75%
-    // of the entries).  (COCOA_HOTRUNS: its hot / cold run classes keep c.)
-    constexpr bool PAR = MIRROR && !COCOA_HOTRUNS;
+    // of the entries, round 5).
+    constexpr bool PAR = MIRROR;
     const int32_t hotc = PAR ? 2 * hot : hot;
     auto hix = [&](int32_t c) -> int32_t { return PAR ? (c >> 1) : c; };
     constexpr int NRUN = MIRROR ? kGramRuns : kGNC;  // partial bases the chain sums
     constexpr int NTH = MIRROR ? kGThreads + 64 : kGThreads;
     const int32_t H = a.H, NB = (H + kGB - 1) / kGB;
-    int role = kRIdle;
-#pragma unroll
-    for (int i = 0; i < kGWaves; ++i)
-        if (wv == i) role = kGRoles[i];
+    int role = C::role(wv);
     if (MIRROR && wv == kGWaves) role = kRRelay;
     role = __builtin_amdgcn_readfirstlane(role);
     const int64_t p0 = a.part_ptr[k];
@@ -1061,7 +1093,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         // the step's inputs one batch ahead (registers)
         const int i = lane & (kGB - 1);
         int32_t xr = nl, xz = 0;
-        int32_t xzc[kGramRuns - 1];  // ends of the column runs 0 .. 2 in the row
+        int32_t xzc[kGramRuns - 1];  // ends of the column runs 0 .. R-2 in the row
         int32_t xpv = -1;            // the step's look-back: latest earlier step of its row in its window (plan)
         double xy = 0.0, xq = 0.0, xxw = 0.0;
         int64_t xbeg = 0;
@@ -1128,7 +1160,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             xpv = -1;
             xy = xq = xxw = 0.0;
             xbeg = 0;
-            if (lane < kGB && j < H) {
+            if (j < H) {  // (every lane: lane group g holds step lane & 15 too; same addresses, coalesced)
                 xr = a.samples[g0 + j];
                 xy = a.plan_y[g0 + j];
                 xq = a.plan_q[g0 + j];
@@ -1140,9 +1172,15 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 xbeg = a.plan_beg[g0 + j];
                 xz = a.plan_z[g0 + j];
                 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-                const i32x4 z4 = *(const i32x4*)(a.plan_zc + 4 * (g0 + j));  // (one 16-byte load)
+                const int32_t* zp = a.plan_zc + (size_t)kGramRuns * (g0 + j);
+                const i32x4 z4 = *(const i32x4*)(zp + kGramRuns - 4);  // (16-byte loads)
+                if (kGramRuns == 8) {
+                    const i32x4 zl = *(const i32x4*)zp;
 #pragma unroll
-                for (int c = 0; c < kGramRuns - 1; ++c) xzc[c] = z4[c];
+                    for (int c = 0; c < 4; ++c) xzc[c] = zl[c];
+                }
+#pragma unroll
+                for (int c = 0; c < 3; ++c) xzc[kGramRuns - 4 + c] = z4[c];
                 xpv = z4[3];
             }
         };
@@ -1166,9 +1204,11 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             // b - kGRing: chain and both memory waves done with it
             if (!wait_ge(&S.cnt[kCChain], b - kGRing + 1, abortf, a.status, pw)) break;
             bool ok = true;
+            if (!all_ge_now(&S.cnt[kCScat], kGNC, min(b, NB) - kGRing + 1)) {
 #pragma unroll
-            for (int c = 0; c < kGNC; ++c)
-                ok = ok && wait_ge(&S.cnt[kCScat + c], min(b, NB) - kGRing + 1, abortf, a.status, pw);
+                for (int c = 0; c < kGNC; ++c)
+                    ok = ok && wait_ge(&S.cnt[kCScat + c], min(b, NB) - kGRing + 1, abortf, a.status, pw);
+            }
             if (!ok) break;
             {
                 const uint64_t td = pw ? __builtin_readcyclecounter() : 0;
@@ -1180,8 +1220,8 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 const int32_t j = b * kGB + i;
                 const bool valid = lane < kGB && j < H;
                 const int32_t r = xr, z = xz, pv = xpv;
-                // class c: entries [beg + ze[c], beg + ze[c+1]) -- runs 2c, 2c+1, or
-                // (mirrored) run 2c + h
+                // class c: entries [beg + zb[c], beg + ze[c+1]) -- runs [c R/2, (c + 1) R/2),
+                // or (mirrored) run 2c + h
                 int32_t zr[kGramRuns + 1];
                 zr[0] = 0;
 #pragma unroll
@@ -1191,8 +1231,8 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
 #pragma unroll
                 for (int c = 0; c < kGNC; ++c) {
                     const int r = gram_mirror_run(c, h);
-                    zb[c] = MIRROR ? zr[r] : zr[2 * c];
-                    ze[c + 1] = MIRROR ? zr[r + 1] : zr[2 * c + 2];
+                    zb[c] = MIRROR ? zr[r] : zr[c * (kGramRuns / 2)];
+                    ze[c + 1] = MIRROR ? zr[r + 1] : zr[(c + 1) * (kGramRuns / 2)];
                 }
                 ze[0] = 0;
                 if (XW && xw_miss) xw_inline();  // (wave-uniform)
@@ -1200,13 +1240,22 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 const int64_t beg = xbeg;
                 if (b + 1 < NB) load(b + 1);
                 lstamp(1);
-                // the rows' runs of each class
-                int32_t inc[kGNC], T[kGNC], nu[kGNC];
+                // the rows' runs of each class, one class per 16-lane row of the wave
+                // (lane group cl = lane >> 4 holds class cl of step lane & 15): one
+                // DPP row scan for all classes
+                const int cl = lane >> 4;
+                int32_t zbl = zb[0], zel = ze[1];
+#pragma unroll
+                for (int c = 1; c < kGNC; ++c)
+                    if (cl == c) {
+                        zbl = zb[c];
+                        zel = ze[c + 1];
+                    }
+                const int32_t incl = row16_incl_scan((cl < kGNC && j < H) ? zel - zbl : 0);
+                int32_t T[kGNC], nu[kGNC];
 #pragma unroll
                 for (int c = 0; c < kGNC; ++c) {
-                    const int32_t zc = ze[c + 1] - zb[c];
-                    inc[c] = wave_incl_scan(lane < kGB ? zc : 0);
-                    T[c] = __shfl(inc[c], kGB - 1, 64);
+                    T[c] = __builtin_amdgcn_readlane(incl, 16 * c + kGB - 1);
                     nu[c] = (T[c] + 63) >> 6;
                 }
                 wave_lds_sync();
@@ -1260,20 +1309,30 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                     R.fwd = 0;
                 }
                 lstamp(4);
+                {
+                    // each lane group its class's layout: one store per field for all classes
+                    int32_t tl = T[0], nl_ = nu[0], pl = nu[0] <= kGMaxU ? cursor[0] : -1;
 #pragma unroll
-                for (int c = 0; c < kGNC; ++c) {
-                    GLay& L = S.lay[b % kGRing][c];
-                    if (lane < kGB) {
-                        L.sx[lane + 1] = inc[c];
-                        L.sb[lane] = beg + zb[c];
+                    for (int c = 1; c < kGNC; ++c)
+                        if (cl == c) {
+                            tl = T[c];
+                            nl_ = nu[c];
+                            pl = nu[c] <= kGMaxU ? cursor[c] : -1;
+                        }
+                    if (cl < kGNC) {
+                        GLay& L = S.lay[b % kGRing][cl];
+                        L.sx[i + 1] = incl;
+                        L.sb[i] = beg + zbl;
+                        if (i == 0) {
+                            L.sx[0] = 0;
+                            L.T = tl;
+                            L.nu = nl_;
+                            L.pos = pl;
+                        }
                     }
-                    if (lane == 0) {
-                        L.sx[0] = 0;
-                        L.T = T[c];
-                        L.nu = nu[c];
-                        L.pos = nu[c] <= kGMaxU ? cursor[c] : -1;
-                    }
-                    if (nu[c] <= kGMaxU) cursor[c] += nu[c] * 64;
+#pragma unroll
+                    for (int c = 0; c < kGNC; ++c)
+                        if (nu[c] <= kGMaxU) cursor[c] += nu[c] * 64;
                 }
                 wave_lds_sync();
                 // mark the earlier occurrence: step pv forwards its new alpha here
@@ -1296,7 +1355,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             lstamp(6);
         }
         if (pw && lane == 0 && h == 0)
-            for (int i = 0; i < 7; ++i) a.prof[(size_t)k * kProfStride + 28 + i] = lph[i];
+            for (int i = 0; i < 7; ++i) a.prof[(size_t)k * kProfStride + 56 + i] = lph[i];
         if (MODE == MODE_LSGD && lane == 0) {  // read after the final barrier
             S.lsgd_s = ls;
             S.lsgd_keep = lkeep;
@@ -1313,7 +1372,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 if (!wait_ge(&S.cnt[kCFreed + c], pos + nu * 64 - kGSub * 64, abortf, a.status, pw)) break;
                 for (int32_t u = 0; u < nu; ++u) {
                     const int32_t q = u * 64 + lane;
-                    uint8_t* ub = S.ring[ring_unit(c, pos, u)];
+                    uint8_t* ub = S.ring[ring_unit<NC>(c, pos, u)];
                     const int o = gram_owner(L.sx, q);
                     if (q < T) {
                         const int64_t e = L.sb[o] + (q - L.sx[o]);
@@ -1359,7 +1418,8 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 tph = t;
             }
         };
-        // KIND 0: a class mixing LDS-resident and slice columns; 1 / 2: the mirrored
+        // KIND 0: a class mixing LDS-resident and slice columns (1 / 2, the round-5
+        // hot-only / cold-only runs of COCOA_HOTRUNS, are gone); the mirrored
         // half's hot-only (LDS) / cold-only (slice) class of the COCOA_HOTRUNS layout
         auto mem_loop = [&](auto kind_c) {
             constexpr int KIND = decltype(kind_c)::value;
@@ -1383,7 +1443,9 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 {
                     const GLay& L = S.lay[b % kGRing][c];
                     const double* cf = S.coef + (b % kGRing) * (2 * kGB);
-                    const int32_t pos = L.pos, nu = L.nu;
+                    const int32_t pos = L.pos, nu_all = L.nu;
+                    // (diag bit 4, timing only: half the units, as if the run were split in two)
+                    const int32_t nu = (COCOA_DIAG_ON && (a.diag & 4)) ? (nu_all + 1) / 2 : nu_all;
                     int32_t scl[kGMaxU];
                     double sp[kGMaxU];
                     if (pos >= 0) {
@@ -1396,7 +1458,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     #pragma unroll
                                 for (int t = 0; t < 4; ++t) {
                                     uint32_t r8;
-                                    ring_get(S, ring_unit(c, pos, u0 + t), lane, scl[u0 + t], vl[t], r8);
+                                    ring_get(S, ring_unit<NC>(c, pos, u0 + t), lane, scl[u0 + t], vl[t], r8);
                                     rw[t] = r8 | gram_pad(u0 + t, nu);
                                 }
     #pragma unroll
@@ -1417,7 +1479,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                     wave_lds_sync();
                     if (COCOA_EARLY_RELEASE && pos >= 0 && lane == 0) {
                         lds_release(&S.cnt[kCScat + c], b + 1);  // coefficient / record / layout slot consumed
-                        lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                        lds_release(&S.cnt[kCFreed + c], pos + nu_all * 64);
                     }
                     if (bases) vm_drain();  // the gathers of batch b+kGNB-1 have read the slice (MbCD: no gathers)
                     stamp(0);
@@ -1438,7 +1500,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                         wave_lds_sync();
                         if (lane == 0) {
                             lds_release(&S.cnt[kCScat + c], b + 1);
-                            if (!COCOA_EARLY_RELEASE && pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu * 64);
+                            if (!COCOA_EARLY_RELEASE && pos >= 0) lds_release(&S.cnt[kCFreed + c], pos + nu_all * 64);
                         }
                     }
                 }
@@ -1480,7 +1542,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 const int32_t x = b + kGNB;
                 if (bases && x < NB) {
                     const GLay& L = S.lay[x % kGRing][c];
-                    const int32_t pos = L.pos, nu = L.nu;
+                    const int32_t pos = L.pos, nu = (COCOA_DIAG_ON && (a.diag & 4)) ? (L.nu + 1) / 2 : L.nu;
                     if (pos >= 0) {
                         if (!fetched(x)) break;
     #pragma unroll
@@ -1495,7 +1557,7 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
     #pragma unroll
                                 for (int t = 0; t < 4; ++t) {
                                     uint32_t r8;
-                                    ring_get(S, ring_unit(c, pos, u0 + t), lane, cl[t], vl[t], r8);
+                                    ring_get(S, ring_unit<NC>(c, pos, u0 + t), lane, cl[t], vl[t], r8);
                                     rw[t] = r8 | gram_pad(u0 + t, nu);
                                 }
                                 double hx[4];
@@ -1556,58 +1618,54 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
                 stamp(2);
             }
         };
-        // (hot_split < hot: the cold class still holds LDS-resident columns: mixed)
-        const bool spec = MIRROR && COCOA_HOTRUNS && HOTLDS && a.hot_split > 0 && a.hot_split <= hot;
-        if (spec && c == 0)
-            mem_loop(std::integral_constant<int, 1>{});
-        else if (spec && a.hot_split == hot)
-            mem_loop(std::integral_constant<int, 2>{});
-        else
-            mem_loop(std::integral_constant<int, 0>{});
+        mem_loop(std::integral_constant<int, 0>{});
         vm_drain();  // the last atomics land before the kernel ends
         if (a.prof && lane == 0)
-            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * kProfStride + 48 + 4 * c + i] = ph[i];
+            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * kProfStride + 64 + 4 * c + i] = ph[i];
     } else if (MIRROR && role == kRRelay) {
         // -------------------------------------------------------- relay --
-        // the other half's partial bases (its runs hp and 2 + hp) of every batch
-        // x >= kGNB, from its tagged granules into this half's LDS
+        // the other half's partial bases (its runs 2 c + hp, c < NC) of every batch
+        // x >= kGNB, from its tagged granules into this half's LDS, two runs per poll
         if (MODE != MODE_MBCD) {
             const int hp = 1 - h;
-            const int run0 = gram_mirror_run(0, hp), run1 = gram_mirror_run(1, hp);
-            const int run = (lane >> 5) ? run1 : run0;  // lanes 0-31: the other half's class 0, 32-63: class 1
             const int row = (lane >> 1) & (kGB - 1), half = lane & 1;
             const uint32_t thi = (uint32_t)(a.xtag_epoch & 0xFFF) << 20;
-            for (int32_t x = kGNB; x < NB; ++x) {
+            bool ok = true;
+            for (int32_t x = kGNB; ok && x < NB; ++x) {
                 // base slot x % kGNB held batch x - kGNB: the chain is done with it
                 if (!wait_ge(&S.cnt[kCChain], x - kGNB + 1, abortf, a.status, pw)) break;
-                uint64_t* gp = a.xbase + (((size_t)k * kGramRuns + run) * kXbR + (x % kXbR)) * (2 * kGB) + (lane & 31);
                 const uint32_t tag = thi | (uint32_t)(x + 1);
-                uint64_t gv = 0;
-                bool ok = true;
-                const uint64_t t0 = pw ? __builtin_readcyclecounter() : 0;
-                for (uint32_t it = 0;; ++it) {  // sc1 polls of the 64 granules until every tag matches
-                    gv = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__all((uint32_t)(gv >> 32) == tag)) break;
-                    if (__hip_atomic_load(abortf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                        ok = false;
-                        break;
+#pragma unroll
+                for (int p = 0; p < NC / 2; ++p) {
+                    const int run0 = gram_mirror_run(2 * p, hp), run1 = gram_mirror_run(2 * p + 1, hp);
+                    const int run = (lane >> 5) ? run1 : run0;  // lanes 0-31: the pair's first run, 32-63: its second
+                    uint64_t* gp = a.xbase + (((size_t)k * kGramRuns + run) * kXbR + (x % kXbR)) * (2 * kGB) + (lane & 31);
+                    uint64_t gv = 0;
+                    const uint64_t t0 = pw ? __builtin_readcyclecounter() : 0;
+                    for (uint32_t it = 0;; ++it) {  // sc1 polls of the 64 granules until every tag matches
+                        gv = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (__all((uint32_t)(gv >> 32) == tag)) break;
+                        if (__hip_atomic_load(abortf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                            ok = false;
+                            break;
+                        }
+                        if (it > (1u << 24)) {
+                            __hip_atomic_store(abortf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (lane == 0) __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            ok = false;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
                     }
-                    if (it > (1u << 24)) {
-                        __hip_atomic_store(abortf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (lane == 0) __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok = false;
-                        break;
+                    if (pw) *pw += __builtin_readcyclecounter() - t0;
+                    if (!ok) break;
+                    const uint32_t mine = (uint32_t)gv, other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+                    if (half == 0) S.base[run][(x % kGNB) * kGB + row] = __hiloint2double((int)other, (int)mine);
+                    wave_lds_sync();
+                    if (lane == 0) {
+                        lds_release(&S.cnt[kCBase + run0], x + 1);
+                        lds_release(&S.cnt[kCBase + run1], x + 1);
                     }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                if (pw) *pw += __builtin_readcyclecounter() - t0;
-                if (!ok) break;
-                const uint32_t mine = (uint32_t)gv, other = (uint32_t)__shfl_xor((int)mine, 1, 64);
-                if (half == 0) S.base[run][(x % kGNB) * kGB + row] = __hiloint2double((int)other, (int)mine);
-                wave_lds_sync();
-                if (lane == 0) {
-                    lds_release(&S.cnt[kCBase + run0], x + 1);
-                    lds_release(&S.cnt[kCBase + run1], x + 1);
                 }
             }
         }
@@ -1633,21 +1691,24 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
             const int q4 = g % kGNB;          // this batch's quarter of the lanes
             const bool mine = lane / kGB == q4;
             if (MODE != MODE_MBCD) {
+                if (!all_ge_now(&S.cnt[kCBase], NRUN, g + 1)) {
 #pragma unroll
-                for (int c = 0; c < NRUN; ++c)
-                    if (!wait_ge(&S.cnt[kCBase + c], g + 1, abortf, a.status,
-                                 !pw ? nullptr
-                                     : (MIRROR && c != gram_mirror_run(0, h) && c != gram_mirror_run(1, h)) ? &wait_base_remote
-                                                                                                               : &wait_base_local))
-                        return false;
+                    for (int c = 0; c < NRUN; ++c)  // (diagnostics: a mirrored half's own runs have parity h)
+                        if (!wait_ge(&S.cnt[kCBase + c], g + 1, abortf, a.status,
+                                     !pw ? nullptr : (MIRROR && (c & 1) != h) ? &wait_base_remote : &wait_base_local))
+                            return false;
+                }
                 if (!wait_ge(&S.cnt[kCLoad], g + ahead, abortf, a.status, pw ? &wait_load : nullptr)) return false;
             } else if (!wait_ge(&S.cnt[kCLoad], min(g + kGNB + 1, NB), abortf, a.status, pw)) {
                 return false;
             }
-            // coefficient ring slot g % kGRing held batch g - kGRing: consumed by both memory waves?
+            // coefficient ring slot g % kGRing held batch g - kGRing: consumed by every memory wave?
+            if (!all_ge_now(&S.cnt[kCScat], kGNC, g - kGRing + 1)) {
 #pragma unroll
-            for (int c = 0; c < kGNC; ++c)
-                if (!wait_ge(&S.cnt[kCScat + c], g - kGRing + 1, abortf, a.status, pw ? &wait_scat : nullptr)) return false;
+                for (int c = 0; c < kGNC; ++c)
+                    if (!wait_ge(&S.cnt[kCScat + c], g - kGRing + 1, abortf, a.status, pw ? &wait_scat : nullptr))
+                        return false;
+            }
             if (MODE != MODE_LSGD) {
                 const int32_t g4 = g + kGNB;
                 const GRec& R4 = S.rec[(g4 % kGRing) * kGB + (lane & (kGB - 1))];
@@ -1762,11 +1823,12 @@ __global__ __launch_bounds__(kGThreads + 64, 1) void solver_gram_kernel(GramSolv
         }
     }
     if (a.prof && lane == 0 && h == 0 && wv < kGWaves) {
-        uint64_t* pr = a.prof + (size_t)k * kProfStride + wv * 4;  // [k][64]: waves at 4 wv, memory phases at 48 + 4 c
+        // [k][128]: waves at 4 wv, chain waits at 48, loader phases at 56, memory phases at 64 + 4 c
+        uint64_t* pr = a.prof + (size_t)k * kProfStride + wv * 4;
         pr[0] = wait_cycles + (role == kRChain ? wait_base_local + wait_base_remote + wait_load + wait_scat : 0);
         if (role == kRChain) {
-            a.prof[(size_t)k * kProfStride + 40] = wait_load;
-            a.prof[(size_t)k * kProfStride + 41] = wait_scat;
+            a.prof[(size_t)k * kProfStride + 48] = wait_load;
+            a.prof[(size_t)k * kProfStride + 49] = wait_scat;
         }
         if (role == kRChain || role == kRLoader) {  // (loader: [2] its vm_drain cycles)
             pr[2] = wait_base_local;

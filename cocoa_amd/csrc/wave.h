@@ -81,6 +81,16 @@ __device__ __forceinline__ int32_t wave_incl_max(int32_t x) {
     return x;
 }
 
+// Inclusive prefix sum of an int within each DPP row of 16 lanes (four
+// independent scans, DPP only: four VALU moves, no LDS round trip).
+__device__ __forceinline__ int32_t row16_incl_scan(int32_t x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    return x;
+}
+
 // Inclusive prefix sum of an int over the wave (all lanes active).
 __device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
     const int l = lane_id();

@@ -34,7 +34,7 @@ def main():
             e.eval()
     e.sync()
     st = e.kernel_stats()
-    S = 64  # kProfStride (kernels.h)
+    S = 128  # kProfStride (kernels.h)
     allp = e.solver_profile_read(e.K_loc * S + 8).astype(np.float64)
     full = allp[:e.K_loc * S].reshape(e.K_loc, S)
     nwg = e.K_loc * ((sh.H + 15) // 16)
@@ -44,8 +44,10 @@ def main():
     gram_phases = dict(zip(names, (allp[e.K_loc * S:e.K_loc * S + 8] / nwg).tolist()))  # per batch (seq: per batch and run)
     # solver_gram.h: [k][64] = wave w at 4 w (wait cycles, total cycles), memory
     # wave c's phase cycles at 48 + 4 c; roles in the default layout (COCOA_GLAYOUT)
-    raw = full[:, :24].reshape(e.K_loc, 6, 4)
-    roles = ["chain", "loader", "memory0", "memory1", "fetch0", "fetch1"]
+    nc = 4 if e.plan().get("gram_mirror") else 2  # column classes (kernels.h kGramRuns / 2 mirrored)
+    roles = ["chain", "loader"] + sum([[f"memory{2*g}", f"memory{2*g+1}", f"fetch{2*g}", f"fetch{2*g+1}"]
+                                        for g in range(nc // 2)], [])
+    raw = full[:, :4 * len(roles)].reshape(e.K_loc, len(roles), 4)
     nb = (sh.H + 15) // 16
     out = {"method": method, "eval_flow": EVAL_FLOW, "plan": e.plan(), "kernel_ms": {k: v["total_ms"] / max(v["launches"], 1) for k, v in st.items()},
            "waves": {r: {"wait_cyc_mean": float(raw[:, i, 0].mean()), "total_cyc_mean": float(raw[:, i, 1].mean()),
@@ -54,17 +56,17 @@ def main():
            "cyc_per_step_chain": float(raw[:, 0, 1].mean() / sh.H),
            "chain_base_wait_frac": {"local": float(raw[:, 0, 2].sum() / max(raw[:, 0, 1].sum(), 1)),
                                     "remote": float(raw[:, 0, 3].sum() / max(raw[:, 0, 1].sum(), 1))},
-           "chain_wait_frac": {"loader": float(full[:, 40].sum() / max(raw[:, 0, 1].sum(), 1)),
-                               "scatter_ring": float(full[:, 41].sum() / max(raw[:, 0, 1].sum(), 1))},
+           "chain_wait_frac": {"loader": float(full[:, 48].sum() / max(raw[:, 0, 1].sum(), 1)),
+                               "scatter_ring": float(full[:, 49].sum() / max(raw[:, 0, 1].sum(), 1))},
            "loader_drain_frac": float(raw[:, 1, 2].sum() / max(raw[:, 1, 1].sum(), 1)),
            "loader_cyc_per_batch": float(raw[:, 1, 1].mean() / nb),
            "loader_phase_cyc_per_batch": dict(zip(["wait_drain", "load_issue", "scans", "forward_search", "records",
                                                    "layouts_marks", "gram_dma_release"],
-                                                  (full[:, 28:35].mean(axis=0) / nb).tolist())),
+                                                  (full[:, 56:63].mean(axis=0) / nb).tolist())),
            "memory_phases_cyc_per_batch": {
-               "memory%d" % c: dict(zip(["products_rowsums", "scatter", "gather_issue", "unused"],
-                                        (full[:, 48 + 4 * c:52 + 4 * c].mean(axis=0) / nb).tolist()))
-               for c in (0, 1)},
+               "memory%d" % c: dict(zip(["drain", "atomics_products", "gather_issue", "scatter_prep"],
+                                        (full[:, 64 + 4 * c:68 + 4 * c].mean(axis=0) / nb).tolist()))
+               for c in range(nc)},
            "gram_phase_cyc_per_wg": gram_phases}
     print(json.dumps(out))
 
