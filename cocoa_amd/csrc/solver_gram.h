@@ -688,12 +688,12 @@ __global__ __launch_bounds__(kGsThreads, 1) void gram_seq_kernel(GramArgs a) {
             // B3: ranks (every wave scans the counts itself) and the pool records
             const int32_t cv = lane < kGsNU * kGsWaves ? L.cnt[lane] : 0;
             const int32_t inc = wave_incl_scan(cv);
-            tot = __shfl(inc, 63, 64);
+            tot = __builtin_amdgcn_readlane(inc, 63);
             ovf = live + tot > kGsPool;
             if (!ovf) {
 #pragma unroll
                 for (int u = 0; u < kGsNU; ++u) {
-                    const int32_t ex = __shfl(inc - cv, u * kGsWaves + wv, 64);
+                    const int32_t ex = __builtin_amdgcn_readlane(inc - cv, uni(u * kGsWaves + wv));
                     if ((m[u] >> lane) & 1) {
                         const int32_t slot = (base + ex + __popcll(m[u] & below)) % kGsPool;
                         const int32_t c = E.col[u];
@@ -743,7 +743,10 @@ __global__ __launch_bounds__(kGsThreads, 1) void gram_seq_kernel(GramArgs a) {
             }
             const GsMetaRec& Mg = L.meta[g & (kGsMeta - 1)];
             const int32_t n = Mg.pn, ps0 = Mg.pstart;
-            for (int32_t i = tid; i < n; i += kGsThreads) {
+            // waves 3.. take the first entries: the MFMA waves walk only what is
+            // left past kGsThreads - 192 (C2: a batch holds ~770 cold entries)
+            const int32_t wt = wv < 3 ? tid + (kGsThreads - 192) : tid - 192;
+            for (int32_t i = wt; i < n; i += kGsThreads) {
                 const int32_t se = (ps0 + i) % kGsPool;
                 const int32_t ecu = L.pcn[se].x;
                 const double ev = L.pval[se];

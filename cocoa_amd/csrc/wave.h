@@ -91,14 +91,13 @@ __device__ __forceinline__ int32_t row16_incl_scan(int32_t x) {
     return x;
 }
 
-// Inclusive prefix sum of an int over the wave (all lanes active).
+// Inclusive prefix sum of an int over the wave (all lanes active): the row
+// scans, then the row_bcast:15 / row_bcast:31 carries as in wave_incl_max.
+// DPP only (the __shfl_up form took six LDS round trips).
 __device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
-    const int l = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (l >= o) x += y;
-    }
+    x = row16_incl_scan(x);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return x;
 }
 
