@@ -854,6 +854,9 @@ constexpr int kGPart = COCOA_GPART;      // product slots per row (lanes l, l + 
 // classes, two memory waves share each of SIMDs 2 and 3).  Waves: chain,
 // loader, then groups of (memory, memory, fetch, fetch); the mirrored form adds
 // the relay as the last wave.
+#ifndef COCOA_GLAY4
+#define COCOA_GLAY4 0  // (eight runs: the four memory waves on four SIMDs, A/B knob)
+#endif
 template <int NC>
 struct GCfg {
     static constexpr int kE = NC == 2 ? 8192 : 4096;
@@ -873,7 +876,10 @@ struct GCfg {
         if (w == 0) return kRChain;
         if (w == 1) return kRLoader;
         if (w >= kWaves) return kRIdle;
-        const int i = w - 2, g = i >> 2, j = i & 3;
+        const int i = w - 2;
+        if (COCOA_GLAY4 && NC == 4)  // the memory waves first: one on each SIMD
+            return i < NC ? kRMem + i : kRFetch + (i - NC);
+        const int g = i >> 2, j = i & 3;
         return j < 2 ? kRMem + 2 * g + j : kRFetch + 2 * g + (j - 2);
     }
 };
@@ -1412,7 +1418,7 @@ void solver_gram_kernel(GramSolverArgs a) {
         int32_t xnu = 0;                //   and its 64-entry units
         double(*part)[kGPart] = S.part[c];
         auto fetched = [&](int32_t x) { return wait_ge(&S.cnt[kCFetch + c], x + 1, abortf, a.status, pw); };
-        uint64_t ph[4] = {0, 0, 0, 0};
+        uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         uint64_t tph = 0;
         auto stamp = [&](int i) {
             if (a.prof) {
@@ -1420,6 +1426,10 @@ void solver_gram_kernel(GramSolverArgs a) {
                 ph[i] += t - tph;
                 tph = t;
             }
+        };
+        // (diagnostic build: the atomics / products phase split in four)
+        auto dstamp = [&](int i) {
+            if (COCOA_DIAG_ON) stamp(i);
         };
         // KIND 0: a class mixing LDS-resident and slice columns (1 / 2, the round-5
         // hot-only / cold-only runs of COCOA_HOTRUNS, are gone); the mirrored
@@ -1490,6 +1500,7 @@ void solver_gram_kernel(GramSolverArgs a) {
     #pragma unroll
                         for (int u = 0; u < kGMaxU; ++u)
                             if (u < nu && scl[u] >= 0 && !(COCOA_DIAG_ON && (a.diag & 1))) dw_addk(scl[u], sp[u]);
+                        dstamp(4);
                     } else {
                         for (int i = 0; i < kGB; ++i) {
                             const double cv = cf[i];
@@ -1517,6 +1528,7 @@ void solver_gram_kernel(GramSolverArgs a) {
                         for (int i = 0; i < kGB; ++i) part[i][lane] = 0.0;
                     }
                     wave_lds_sync();
+                    dstamp(5);
     #pragma unroll
                     for (int u = 0; u < kGMaxU; ++u) {
                         if (u < xnu) {
@@ -1526,6 +1538,7 @@ void solver_gram_kernel(GramSolverArgs a) {
                         }
                     }
                     wave_lds_sync();
+                    dstamp(6);
                     const int rr = lane >> 2, qq = (lane & 3) * (kGPart / 4);
                     double s4 = 0.0;
     #pragma unroll
@@ -1548,6 +1561,7 @@ void solver_gram_kernel(GramSolverArgs a) {
                     const int32_t pos = L.pos, nu = (COCOA_DIAG_ON && (a.diag & 4)) ? (L.nu + 1) / 2 : L.nu;
                     if (pos >= 0) {
                         if (!fetched(x)) break;
+                        dstamp(7);
     #pragma unroll
                         for (int w = 0; w < (kGMaxU + 5) / 6; ++w) hrow[w] = 0xFFFFFFFFu;  // units past nu: never read
                         // groups of 4 units (a group past the batch is skipped whole)
@@ -1623,8 +1637,11 @@ void solver_gram_kernel(GramSolverArgs a) {
         };
         mem_loop(std::integral_constant<int, 0>{});
         vm_drain();  // the last atomics land before the kernel ends
-        if (a.prof && lane == 0)
+        if (a.prof && lane == 0) {
             for (int i = 0; i < 4; ++i) a.prof[(size_t)k * kProfStride + 64 + 4 * c + i] = ph[i];
+            if (COCOA_DIAG_ON && c < 2)
+                for (int i = 4; i < 8; ++i) a.prof[(size_t)k * kProfStride + 96 + 4 * c + i - 4] = ph[i];
+        }
     } else if (MIRROR && role == kRRelay) {
         // -------------------------------------------------------- relay --
         // the other half's partial bases (its runs 2 c + hp, c < NC) of every batch
@@ -1686,6 +1703,17 @@ void solver_gram_kernel(GramSolverArgs a) {
             if (PROJ) R.AA = aa;
         }
         wave_lds_sync();
+        // (diagnostic build: the chain's cycles per part of a batch -- waits, head
+        // loads, the 16 steps, the tail)
+        uint64_t cph[4] = {0, 0, 0, 0};
+        uint64_t ctp = (COCOA_DIAG_ON && pw) ? __builtin_readcyclecounter() : 0;
+        auto cstamp = [&](int i) {
+            if (COCOA_DIAG_ON && pw) {
+                const uint64_t t = __builtin_readcyclecounter();
+                cph[i] += t - ctp;
+                ctp = t;
+            }
+        };
         // One batch.  Alpha of batch g+3 is loaded at the start of batch g (rows met
         // again in batches g .. g+3 are forwarded instead) and written into its
         // records at the end of batch g+1, a batch after the load: `aissue` / `afill`
@@ -1712,6 +1740,7 @@ void solver_gram_kernel(GramSolverArgs a) {
                     if (!wait_ge(&S.cnt[kCScat + c], g - kGRing + 1, abortf, a.status, pw ? &wait_scat : nullptr))
                         return false;
             }
+            cstamp(0);
             if (MODE != MODE_LSGD) {
                 const int32_t g4 = g + kGNB;
                 const GRec& R4 = S.rec[(g4 % kGRing) * kGB + (lane & (kGB - 1))];
@@ -1748,6 +1777,7 @@ void solver_gram_kernel(GramSolverArgs a) {
             }
             lgkm_drain();  // records and Gram rows in: no LDS wait inside the steps
             const uint32_t fwm = (uint32_t)(__ballot(mine && rF >= 0) >> slot0) & 0xFFFFu;  // steps that forward
+            cstamp(1);
             // 16 steps, padding steps included (their record is inert: B = Y = YA = 0,
             // row = the sink).  Step i: nt = clamp(AE - B sdot) with sdot = acc on its
             // lane; c = Y nt - YA; acc += c G(., j).  Lanes of steps <= i have G = 0, so
@@ -1790,6 +1820,7 @@ void solver_gram_kernel(GramSolverArgs a) {
                     }
                 }
             }
+            cstamp(2);
             if (MODE == MODE_LSGD) {
                 const double ev = fma(-rB, acc, rAE);
                 if (mine) cfo[lane & (kGB - 1)] = ev > 0.0 ? rY : 0.0;
@@ -1817,6 +1848,7 @@ void solver_gram_kernel(GramSolverArgs a) {
                 }
             }
             wave_lds_sync();
+            cstamp(3);
             return true;
         };
         double aA = 0.0, aB = 0.0;
@@ -1824,6 +1856,8 @@ void solver_gram_kernel(GramSolverArgs a) {
             if (!batch(g, aA, aB)) break;
             if (g + 1 < NB && !batch(g + 1, aB, aA)) break;
         }
+        if (COCOA_DIAG_ON && pw && lane == 0 && h == 0)
+            for (int i = 0; i < 4; ++i) a.prof[(size_t)k * kProfStride + 50 + i] = cph[i];
     }
     if (a.prof && lane == 0 && h == 0 && wv < kGWaves) {
         // [k][128]: waves at 4 wv, chain waits at 48, loader phases at 56, memory phases at 64 + 4 c

@@ -1,0 +1,11 @@
+#!/bin/bash
+# memory wave: the gather's wait for the fetch wave (diag build)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+O=gpurun_out
+T=${TAG:-r09g}
+for dg in 0; do
+COCOA_GRAM_DIAG=$dg COCOA_LIB=build/diag/libcocoa_hip.so timeout -k 10 200 python3 tools/prof_gram.py cocoa+ --eval > $O/profsolver_${T}_d$dg.json 2> $O/profsolver_${T}_d$dg.err || exit $?
+python3 -c "import json;d=json.load(open('$O/profsolver_${T}_d$dg.json'));print('diag $dg', round(d['kernel_ms']['solver'],4), {k: round(v) for k, v in d['chain_phase_cyc_per_batch'].items()}, {k: round(v) for k, v in d['memory_phases_cyc_per_batch']['memory0'].items()}, {k: round(v) for k, v in d['memory_split_cyc_per_batch']['memory0'].items()}, d['waves'])"
+done

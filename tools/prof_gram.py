@@ -58,6 +58,8 @@ def main():
                                     "remote": float(raw[:, 0, 3].sum() / max(raw[:, 0, 1].sum(), 1))},
            "chain_wait_frac": {"loader": float(full[:, 48].sum() / max(raw[:, 0, 1].sum(), 1)),
                                "scatter_ring": float(full[:, 49].sum() / max(raw[:, 0, 1].sum(), 1))},
+           "chain_phase_cyc_per_batch": dict(zip(["waits", "head_loads", "steps", "tail"],
+                                                 (full[:, 50:54].mean(axis=0) / nb).tolist())),
            "loader_drain_frac": float(raw[:, 1, 2].sum() / max(raw[:, 1, 1].sum(), 1)),
            "loader_cyc_per_batch": float(raw[:, 1, 1].mean() / nb),
            "loader_phase_cyc_per_batch": dict(zip(["wait_drain", "load_issue", "scans", "forward_search", "records",
@@ -67,6 +69,10 @@ def main():
                "memory%d" % c: dict(zip(["drain", "atomics_products", "gather_issue", "scatter_prep"],
                                         (full[:, 64 + 4 * c:68 + 4 * c].mean(axis=0) / nb).tolist()))
                for c in range(nc)},
+           "memory_split_cyc_per_batch": {
+               "memory%d" % c: dict(zip(["scatter_atomics", "part_zero", "part_adds", "gather_fetch_wait"],
+                                        (full[:, 96 + 4 * c:100 + 4 * c].mean(axis=0) / nb).tolist()))
+               for c in range(2)},
            "gram_phase_cyc_per_wg": gram_phases}
     print(json.dumps(out))
 
