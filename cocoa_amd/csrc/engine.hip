@@ -337,10 +337,11 @@ struct cocoa_ctx {
     // coefficients.  csc_ready: built for the current training set.
     // fast evaluation split by column (EvalArgs::row_base): the train rows'
     // entries in device columns < kEvalHot (hot CSR, 16-bit columns) and the rest
-    // (cold CSR), with tiles for each, and the hot pass's per-row dots
-    Csr hot_tr, cold_tr;
-    DevBuf hot_tiles, cold_tiles, row_base;
-    int64_t n_hot_tiles = 0, n_cold_tiles = 0;
+    // (cold CSR), with tiles for each, and the hot pass's per-row dots; for d past
+    // kEvalHot + kEvalWarm the warm columns in a third CSR (16-bit offsets)
+    Csr hot_tr, cold_tr, warm_tr;
+    DevBuf hot_tiles, cold_tiles, warm_tiles, row_base;
+    int64_t n_hot_tiles = 0, n_cold_tiles = 0, n_warm_tiles = 0;
     bool split_ready = false;
     DevBuf csc_ptr, csc_row, csc_val, csc_tiles, row_cnt, row_c;
     int64_t n_csc_tiles = 0;
@@ -1018,25 +1019,41 @@ extern "C" int cocoa_set_train(cocoa_ctx* ctx, int32_t num_parts, const int64_t*
 // The fast evaluation's hot / cold split of the train rows (EvalArgs::row_base):
 // entries of device columns < kEvalHot into one CSR (16-bit columns), the rest
 // into another, each row's entries in stored order, and eval tiles for both.
-// COCOA_EVAL_SPLIT=0 keeps the one-pass evaluation.
+// With d > kEvalHot + kEvalWarm (C4) the columns [kEvalHot, kEvalHot +
+// kEvalWarm) get a CSR of their own (16-bit offsets), the warm tier; the cold
+// CSR then holds the columns past it.  Measured on C4 it gains nothing (1.107
+// against 1.101-1.106 ms, profiles/r06/ab_r09j_c4_warm.txt): the cold pass is
+// bound by its gather instructions, not by where w lives, so the warm tier is
+// built only with COCOA_EVAL_WARM=1.  COCOA_EVAL_SPLIT=0 keeps the one-pass
+// evaluation.
 static void build_eval_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::vector<int32_t>& pcol,
                              const double* val, int64_t n, int32_t d, hipStream_t s) {
     const char* se = std::getenv("COCOA_EVAL_SPLIT");
     ctx->split_ready = false;
     ctx->hot_tr = Csr{};
     ctx->cold_tr = Csr{};
+    ctx->warm_tr = Csr{};
+    ctx->n_warm_tiles = 0;
     if ((se && !std::atoi(se)) || ctx->strict || n < 1) return;
-    std::vector<int64_t> hp((size_t)n + 1), cp((size_t)n + 1);
-    hp[0] = cp[0] = 0;
+    const char* sw = std::getenv("COCOA_EVAL_WARM");
+    // warm tier end (columns below it and past kEvalHot); kEvalHot: none
+    const int32_t wend = (sw && std::atoi(sw) && d > kEvalHot + kEvalWarm) ? kEvalHot + kEvalWarm : kEvalHot;
+    std::vector<int64_t> hp((size_t)n + 1), cp((size_t)n + 1), mp((size_t)n + 1);
+    hp[0] = cp[0] = mp[0] = 0;
     for (int64_t r = 0; r < n; ++r) {
-        int64_t h = 0;
-        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) h += pcol[(size_t)q] < kEvalHot;
+        int64_t h = 0, m = 0;
+        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) {
+            h += pcol[(size_t)q] < kEvalHot;
+            m += pcol[(size_t)q] >= kEvalHot && pcol[(size_t)q] < wend;
+        }
         hp[(size_t)r + 1] = hp[(size_t)r] + h;
-        cp[(size_t)r + 1] = cp[(size_t)r] + (row_ptr[r + 1] - row_ptr[r] - h);
+        mp[(size_t)r + 1] = mp[(size_t)r] + m;
+        cp[(size_t)r + 1] = cp[(size_t)r] + (row_ptr[r + 1] - row_ptr[r] - h - m);
     }
-    const int64_t nh = hp[(size_t)n], nc = cp[(size_t)n];
-    std::vector<uint16_t> hc((size_t)std::max<int64_t>(nh, 1));
+    const int64_t nh = hp[(size_t)n], nc = cp[(size_t)n], nm = mp[(size_t)n];
+    std::vector<uint16_t> hc((size_t)std::max<int64_t>(nh, 1)), mc((size_t)std::max<int64_t>(nm, 1));
     std::vector<double> hv((size_t)std::max<int64_t>(nh, 1)), cv((size_t)std::max<int64_t>(nc, 1));
+    std::vector<double> mv((size_t)std::max<int64_t>(nm, 1));
     std::vector<int32_t> cc((size_t)std::max<int64_t>(nc, 1));
     // each part of a row in ascending device column: neighbouring lanes of a gather
     // then read neighbouring words of w (fewer lines per gather instruction, fewer
@@ -1053,11 +1070,14 @@ static void build_eval_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::
                                  [](const std::pair<int32_t, double>& x, const std::pair<int32_t, double>& y) {
                                      return x.first < y.first;
                                  });
-                int64_t a = hp[(size_t)r], b = cp[(size_t)r];
+                int64_t a = hp[(size_t)r], b = cp[(size_t)r], m = mp[(size_t)r];
                 for (const auto& cvp : tmp) {
                     if (cvp.first < kEvalHot) {
                         hc[(size_t)a] = (uint16_t)cvp.first;
                         hv[(size_t)a++] = cvp.second;
+                    } else if (cvp.first < wend) {
+                        mc[(size_t)m] = (uint16_t)(cvp.first - kEvalHot);
+                        mv[(size_t)m++] = cvp.second;
                     } else {
                         cc[(size_t)b] = cvp.first;
                         cv[(size_t)b++] = cvp.second;
@@ -1080,6 +1100,14 @@ static void build_eval_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::
     eval_split_tiles(&hcap, &ccap);
     ctx->n_hot_tiles = make_tiles(hp.data(), n, ctx->hot_tiles, s, hcap);    // (synchronises)
     ctx->n_cold_tiles = make_tiles(cp.data(), n, ctx->cold_tiles, s, ccap);
+    if (wend > kEvalHot) {
+        ctx->warm_tr.n = n;
+        ctx->warm_tr.nnz = nm;
+        upload(ctx->warm_tr.row_ptr, mp.data(), sizeof(int64_t) * (size_t)(n + 1), s);
+        upload_padded(ctx->warm_tr.col16, mc.data(), sizeof(uint16_t) * (size_t)nm, s);
+        upload_padded(ctx->warm_tr.val, mv.data(), sizeof(double) * (size_t)nm, s);
+        ctx->n_warm_tiles = make_tiles(mp.data(), n, ctx->warm_tiles, s, hcap);  // (synchronises)
+    }
     ctx->row_base.alloc(sizeof(double) * (size_t)n);
     ctx->split_ready = true;
 }
@@ -2436,6 +2464,13 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
         e.val = ctx->cold_tr.val.as<double>();
         e.tiles = ctx->cold_tiles.as<int64_t>();
         e.n_tiles = ctx->n_cold_tiles;
+        if (ctx->n_warm_tiles > 0) {
+            e.m_row_ptr = ctx->warm_tr.row_ptr.as<int64_t>();
+            e.m_col16 = ctx->warm_tr.col16.as<uint16_t>();
+            e.m_val = ctx->warm_tr.val.as<double>();
+            e.m_tiles = ctx->warm_tiles.as<int64_t>();
+            e.n_m_tiles = ctx->n_warm_tiles;
+        }
     }
     ctx->timed_on(st, COCOA_K_EVAL, [&] {
         if (ctx->strict)
@@ -3667,7 +3702,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
                   "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d,"
-                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld,\"mbsgd_pull\":%d,\"eval_split\":%d}",
+                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld,\"mbsgd_pull\":%d,\"eval_split\":%d,\"eval_warm\":%d}",
                   ctx->use_gram ? ctx->gram_chunks : 0, ctx->gram_mirror && !ctx->device_shared() ? 1 : 0,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
@@ -3677,7 +3712,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
                   ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot, ctx->dw_priv ? 1 : 0,
                   (long long)ctx->max_uh, (long long)ctx->n_tail, ctx->mbsgd_pull ? 1 : 0,
-                  ctx->split_ready && !ctx->strict ? 1 : 0);
+                  ctx->split_ready && !ctx->strict ? 1 : 0, ctx->split_ready && ctx->n_warm_tiles > 0 ? 1 : 0);
     require(wrote >= 0 && wrote < len, COCOA_E_ARG, "cocoa_plan_info: buffer too small");
     CAPI_END(ctx)
 }

@@ -22,16 +22,17 @@ constexpr int kWave = 64;
 // classes, class lc taking the runs [lc R/2, (lc + 1) R/2); the mirrored
 // solver's half h (two workgroups per partition) has R/2 classes, class lc
 // taking run 2 lc + h, so half h owns the columns of parity h.
-// COCOA_RUNS=8 (round 6, measured and not the default): each mirrored half then
-// has four memory waves, each with half the units per batch.  A diag build
-// with half the units per memory wave had shown the solver 2.03 -> 1.60 ms;
-// with eight runs, the loader's per-class work vectorised and the counters read
-// at once, the C2 solver measured 1.727-1.729 against 1.745-1.752 ms for four
-// runs on one box, but the step did not move (2.008-2.010 against 1.998-2.005
-// ms): the next round's Gram rows, 1.61 ms beside the solver, then still run
-// into the evaluation.
+// Eight runs (the default since round 6's last tree): each mirrored half has
+// four memory waves, each with half the units per batch of the four-run form.
+// A diag build with half the units per memory wave had shown the solver 2.03
+// -> 1.60 ms; with eight runs, the loader's per-class work vectorised and the
+// counters read at once, the C2 solver measures 1.721-1.724 against
+// 1.737-1.745 ms for four runs, and the step 1.975-1.977 against 1.992-1.998
+// ms on one box (profiles/r06/ab_r09h.txt; with the round-6 Gram rows at 1.6
+// ms the step had not moved, as they then ran into the evaluation).
+// COCOA_RUNS=4 builds the four-run form.
 #ifndef COCOA_RUNS
-#define COCOA_RUNS 4
+#define COCOA_RUNS 8
 #endif
 constexpr int kGramRuns = COCOA_RUNS;  // column runs of a fast-mode row
 static_assert(kGramRuns == 4 || kGramRuns == 8, "column runs");
@@ -309,8 +310,18 @@ struct EvalArgs {
     const int64_t* h_tiles;
     int64_t n_h_tiles;
     double* row_base;
+    // wide d (> kEvalHot + kEvalWarm): the warm entries (device columns [kEvalHot,
+    // kEvalHot + kEvalWarm), 16-bit offsets from kEvalHot) as a third CSR, summed
+    // into row_base by a pass whose w gathers stay in L2; the cold CSR then holds
+    // the columns past them.  n_m_tiles 0: no warm pass
+    const int64_t* m_row_ptr;
+    const uint16_t* m_col16;
+    const double* m_val;
+    const int64_t* m_tiles;
+    int64_t n_m_tiles;
 };
-constexpr int kEvalHot = 4096;  // w columns in LDS in the split evaluation's hot pass
+constexpr int kEvalHot = 4096;   // w columns in LDS in the split evaluation's hot pass
+constexpr int kEvalWarm = 65536; // columns of its warm pass (0.5 MB of w: L2-resident gathers)
 void eval_split_tiles(int* hot_cap, int* cold_cap);  // tile entries of its hot / cold passes
 
 // fast translation unit

@@ -600,38 +600,49 @@ int eval_tile_entries(int64_t d) { return d > kEvalWideD ? 2048 : kEvalTile; }
 // (eval_stream_kernel<..., BASE>) then streams the remaining entries with global
 // gathers, adds row_base and does the hinge / error / alpha / ||w|| sums.  Tiles
 // and loads as in eval_stream_kernel.
-template <int TILE, int BLOCK, int HOT>
+// WARM: the warm pass over the third CSR (EvalArgs::m_*): w gathered from global
+// memory at kEvalHot + the 16-bit offset (a 0.5 MB slice, L2-resident), each
+// row's dot added to the hot pass's row_base (staged per tile, like the labels
+// of eval_stream_kernel)
+template <int TILE, int BLOCK, int HOT, bool WARM = false>
 __global__ __launch_bounds__(BLOCK) void eval_hot_kernel(EvalArgs a) {
     constexpr int UNITS = TILE / (4 * BLOCK);
     __shared__ double prod[TILE + 4];
     __shared__ uint16_t roff[TILE + 2];
     __shared__ double red[BLOCK / 64];
-    __shared__ double whot[HOT];
+    __shared__ double whot[WARM ? 1 : HOT];
+    __shared__ double bl[WARM ? kEvalRows : 1];
     const int tid = threadIdx.x;
-    {
+    if (!WARM) {
         const int32_t h = (int32_t)min<int64_t>(HOT, a.d);
         for (int32_t j = tid; j < HOT; j += BLOCK) whot[j] = j < h ? a.w[j] : 0.0;
         __syncthreads();
     }
+    const gdouble* wm = (const gdouble*)(a.w + kEvalHot);
+    auto w_of = [&](int32_t c) -> double { return WARM ? wm[c] : whot[c]; };
     const int sub = tid & 15, grp = tid >> 4;
-    const int64_t* tl = a.h_tiles;
-    const int64_t* te = tl + a.n_h_tiles + 1;
-    const int64_t* rp = a.h_row_ptr;
-    const uint16_t* cl = a.h_col16;
-    const double* vl = a.h_val;
-    for (int64_t t = blockIdx.x; t < a.n_h_tiles; t += gridDim.x) {
+    const int64_t nt = WARM ? a.n_m_tiles : a.n_h_tiles;
+    const int64_t* tl = WARM ? a.m_tiles : a.h_tiles;
+    const int64_t* te = tl + nt + 1;
+    const int64_t* rp = WARM ? a.m_row_ptr : a.h_row_ptr;
+    const uint16_t* cl = WARM ? a.m_col16 : a.h_col16;
+    const double* vl = WARM ? a.m_val : a.h_val;
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
         const int64_t r0 = tl[t], r1 = tl[t + 1];
         const int64_t e0 = te[t], e1 = te[t + 1];
         const int64_t T = e1 - e0;
         if (T > TILE) {
             double acc = 0.0;
-            for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += vl[q] * whot[cl[q]];
+            for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += vl[q] * w_of(cl[q]);
             const double dot = block_sum_n<BLOCK>(acc, red);
-            if (tid == 0) a.row_base[r0] = dot;
+            if (tid == 0) a.row_base[r0] = WARM ? a.row_base[r0] + dot : dot;
             continue;
         }
         const int nr = (int)(r1 - r0);
-        for (int i = tid; i <= nr; i += BLOCK) roff[i] = (uint16_t)(rp[r0 + i] - e0);
+        for (int i = tid; i <= nr; i += BLOCK) {
+            roff[i] = (uint16_t)(rp[r0 + i] - e0);
+            if (WARM && i < nr) bl[i] = a.row_base[r0 + i];
+        }
         const int64_t base = e0 & ~(int64_t)3;
         const int sh = (int)(e0 - base);
         const int64_t span = e1 - base;
@@ -653,8 +664,8 @@ __global__ __launch_bounds__(BLOCK) void eval_hot_kernel(EvalArgs a) {
         for (int u = 0; u <= UNITS; ++u) {
             const int64_t k = 4 * ((int64_t)u * BLOCK + tid);
             if (k < span) {
-                *(f64x2*)(prod + k) = f64x2{v0[u].x * whot[c[u].x], v0[u].y * whot[c[u].y]};
-                *(f64x2*)(prod + k + 2) = f64x2{v1[u].x * whot[c[u].z], v1[u].y * whot[c[u].w]};
+                *(f64x2*)(prod + k) = f64x2{v0[u].x * w_of(c[u].x), v0[u].y * w_of(c[u].y)};
+                *(f64x2*)(prod + k + 2) = f64x2{v1[u].x * w_of(c[u].z), v1[u].y * w_of(c[u].w)};
             }
         }
         __syncthreads();
@@ -663,7 +674,7 @@ __global__ __launch_bounds__(BLOCK) void eval_hot_kernel(EvalArgs a) {
             double acc = 0.0;
             for (int q = b + sub; q < e; q += 16) acc += prod[q];
             const double dot = row16_sum(acc);
-            if (sub == 0) a.row_base[r0 + r] = dot;
+            if (sub == 0) a.row_base[r0 + r] = WARM ? bl[r] + dot : dot;
         }
         __syncthreads();
     }
@@ -711,6 +722,11 @@ static bool launch_eval_split(const EvalArgs& a, int blocks, hipStream_t s) {
     const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
     const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_h_tiles, 256 * COCOA_HOT_WGS));
     eval_hot_kernel<COCOA_HOT_TILE, COCOA_HOT_BLOCK, kEvalHot><<<hb, COCOA_HOT_BLOCK, 0, s>>>(a);
+    if (a.n_m_tiles > 0) {
+        const int mb = resident_grid(eval_hot_kernel<COCOA_HOT_TILE, COCOA_HOT_BLOCK, kEvalHot, true>, COCOA_HOT_BLOCK,
+                                     (int)std::max<int64_t>(1, std::min<int64_t>(a.n_m_tiles, 256 * 8)));
+        eval_hot_kernel<COCOA_HOT_TILE, COCOA_HOT_BLOCK, kEvalHot, true><<<mb, COCOA_HOT_BLOCK, 0, s>>>(a);
+    }
     if (c16) {
         blocks = resident_grid(eval_stream_kernel<COCOA_COLD_TILE, COCOA_COLD_BLOCK, true, 0, 0, true>, COCOA_COLD_BLOCK,
                                blocks);

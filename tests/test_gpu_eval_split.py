@@ -6,7 +6,10 @@ hinge / alpha / ||w|| / test-error sums (OptUtils.scala:57-98).  Checked
 against the oracle and the one-pass evaluation (COCOA_EVAL_SPLIT=0) on the same
 (w, alpha): C2 and C4-shaped rows (16-bit and 32-bit cold columns), rows longer
 than a tile in either part (a 5,000-entry row of duplicate hot columns), empty
-rows, and the next round's plan reading the x.w it stored."""
+rows, and the next round's plan reading the x.w it stored.  Wide d (C4) adds
+the warm tier (COCOA_EVAL_WARM=1, measured and not the default): columns
+[4,096, 69,632) in a CSR of their own, summed into the row dots by a pass
+whose w gathers stay in L2."""
 import numpy as np
 import pytest
 
@@ -28,11 +31,13 @@ def _state(tr, H, lam, rounds=3):
     return run
 
 
-def _eval(monkeypatch, tr, te, run, H, lam, split):
+def _eval(monkeypatch, tr, te, run, H, lam, split, warm=False):
     monkeypatch.setenv("COCOA_EVAL_SPLIT", "1" if split else "0")
+    monkeypatch.setenv("COCOA_EVAL_WARM", "1" if warm else "0")
     e = Engine(strict=False)
     e.set_train(tr)
     monkeypatch.delenv("COCOA_EVAL_SPLIT")
+    monkeypatch.delenv("COCOA_EVAL_WARM")
     e.set_test(te)
     e.init("cocoa+", tr.n, 0, H, lam)
     e.set_w(run.w())
@@ -74,10 +79,54 @@ def test_split_eval_matches_oracle_and_one_pass(data, monkeypatch):
     rv = run.eval(odata(te))
     e1, ev1 = _eval(monkeypatch, tr, te, run, H, lam, True)
     e0, ev0 = _eval(monkeypatch, tr, te, run, H, lam, False)
+    assert e1.plan()["eval_warm"] == 0
     _check(ev1, rv, 1e-12)
     _check(ev0, rv, 1e-12)
     for k in ("primal", "dual", "gap"):
         assert abs(ev1[k] - ev0[k]) <= 1e-13 * abs(rv["primal"])
+    if data == "c4":  # three tiers (COCOA_EVAL_WARM=1) on the same data
+        e2, ev2 = _eval(monkeypatch, tr, te, run, H, lam, True, warm=True)
+        assert e2.plan()["eval_warm"] == 1
+        _check(ev2, rv, 1e-12)
+
+
+def _warm_rows():
+    """Rows whose device columns fill all three tiers: 4,096 frequent columns
+    (hot), 5,000 of medium frequency (warm) and ~70 k singletons (warm up to
+    device column 69,632, cold past it); a row with all 5,000 medium columns
+    (its warm part alone passes the 4,096-entry tile), rows with no medium
+    columns, and an empty row."""
+    rng = np.random.default_rng(11)
+    d = 300000
+    rows = []
+    for i in range(1500):
+        parts = [rng.integers(0, 4096, size=20), rng.integers(9096, d, size=55)]
+        if i % 7:
+            parts.append(rng.integers(4096, 9096, size=12))
+        if i == 5:
+            parts.append(np.arange(4096, 9096))
+        cols = np.unique(np.concatenate(parts)) if i != 3 else np.zeros(0, np.int64)
+        rows.append(cols)
+    row_ptr = np.zeros(len(rows) + 1, np.int64)
+    row_ptr[1:] = np.cumsum([len(c) for c in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.standard_normal(len(col)) / 10.0
+    y = np.where(rng.random(len(rows)) < 0.5, -1.0, 1.0)
+    part = np.array([0, 375, 750, 1125, 1500], np.int64)
+    return LabeledData(row_ptr, col, val, y, part, d)
+
+
+def test_warm_tier_edges_match_oracle(monkeypatch):
+    tr = _warm_rows()
+    te = tr.row_range(100, 900)
+    run = _state(tr, 150, 2e-3)
+    rv = run.eval(odata(te))
+    e1, ev1 = _eval(monkeypatch, tr, te, run, 150, 2e-3, True, warm=True)
+    assert e1.plan()["eval_warm"] == 1
+    e2, ev2 = _eval(monkeypatch, tr, te, run, 150, 2e-3, True)
+    assert e2.plan()["eval_warm"] == 0
+    _check(ev1, rv, 1e-12)
+    _check(ev2, rv, 1e-12)
 
 
 def test_split_eval_xw_feeds_the_next_round(monkeypatch):
