@@ -16,6 +16,9 @@ export TMPDIR=/tmp
 TAG=${TAG:-now}
 O=gpurun_out
 SHORT="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-gap ${BENCH_ARGS}"
+# the prof step profiles the bench's own window (20 warmup + 50 timed rounds), so the
+# kernels' averages over launches 21.. are the timed window bench.py's HIP events see
+PROFRUN="python3 bench.py --steps 50 --warmup 20 --no-cpu-baseline --no-gap ${BENCH_ARGS}"
 
 line() {  # name, args...
   local n=$1; shift
@@ -37,9 +40,9 @@ for step in "$@"; do
       timeout -k 10 600 python3 bench.py ${BENCH_ARGS} > $O/bench_$TAG.json 2> $O/bench_$TAG.err || exit $?
       tail -1 $O/bench_$TAG.json ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_$TAG -o run --output-format csv -- $SHORT \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/rocprof_$TAG -o run --output-format csv -- $PROFRUN \
         > $O/rocprof_$TAG.log 2>&1 || exit $?
-      python3 tools/rocprof_stats.py $O/rocprof_$TAG ;;
+      python3 tools/rocprof_stats.py $O/rocprof_$TAG 20 | tee $O/rocprof_window_$TAG.txt ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 120 rocprofv3 --pmc $c -d $O/pmc_${c}_$TAG -o run --output-format csv -- $SHORT \
