@@ -343,6 +343,12 @@ struct cocoa_ctx {
     DevBuf hot_tiles, cold_tiles, warm_tiles, row_base;
     int64_t n_hot_tiles = 0, n_cold_tiles = 0, n_warm_tiles = 0;
     bool split_ready = false;
+    // the test rows split the same way (te_split: built by cocoa_set_test on a
+    // split training set); row_base then holds n + n_test dots
+    Csr hot_te, cold_te;
+    DevBuf hot_t_tiles, cold_t_tiles;
+    int64_t n_hot_t_tiles = 0, n_cold_t_tiles = 0;
+    bool te_split = false;
     DevBuf csc_ptr, csc_row, csc_val, csc_tiles, row_cnt, row_c;
     int64_t n_csc_tiles = 0;
     bool csc_ready = false;
@@ -1030,6 +1036,7 @@ static void build_eval_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::
                              const double* val, int64_t n, int32_t d, hipStream_t s) {
     const char* se = std::getenv("COCOA_EVAL_SPLIT");
     ctx->split_ready = false;
+    ctx->te_split = false;  // (row_base is re-sized below; cocoa_set_test splits the test rows again)
     ctx->hot_tr = Csr{};
     ctx->cold_tr = Csr{};
     ctx->warm_tr = Csr{};
@@ -1112,6 +1119,67 @@ static void build_eval_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::
     ctx->split_ready = true;
 }
 
+// The test rows' hot / cold split (EvalArgs::th_*), on a split training set:
+// each test row's entries of device columns < kEvalHot go to the hot pass (w
+// from LDS, no gather; their dot into row_base[n + r]), the rest stay in the
+// cold pass's test tiles.  C2's 50,000 test rows hold 3.8 M entries, 78% of
+// them hot: unsplit, the cold pass gathered w for all of them.  Each part in
+// ascending device column, like the train split (the sums are reassociated).
+static void build_test_split(cocoa_ctx* ctx, const int64_t* row_ptr, const std::vector<int32_t>& pcol,
+                             const double* val, int64_t n, hipStream_t s) {
+    ctx->te_split = false;
+    const char* ts = std::getenv("COCOA_EVAL_TEST_SPLIT");  // (=0: the test rows whole in the cold pass)
+    if (!ctx->split_ready || ctx->strict || n < 1 || (ts && !std::atoi(ts))) return;
+    std::vector<int64_t> hp((size_t)n + 1), cp((size_t)n + 1);
+    hp[0] = cp[0] = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t h = 0;
+        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) h += pcol[(size_t)q] < kEvalHot;
+        hp[(size_t)r + 1] = hp[(size_t)r] + h;
+        cp[(size_t)r + 1] = cp[(size_t)r] + (row_ptr[r + 1] - row_ptr[r] - h);
+    }
+    const int64_t nh = hp[(size_t)n], nc = cp[(size_t)n];
+    std::vector<uint16_t> hc((size_t)std::max<int64_t>(nh, 1));
+    std::vector<double> hv((size_t)std::max<int64_t>(nh, 1)), cv((size_t)std::max<int64_t>(nc, 1));
+    std::vector<int32_t> cc((size_t)std::max<int64_t>(nc, 1));
+    std::vector<std::pair<int32_t, double>> tmp;
+    for (int64_t r = 0; r < n; ++r) {
+        tmp.clear();
+        for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) tmp.emplace_back(pcol[(size_t)q], val[q]);
+        std::stable_sort(tmp.begin(), tmp.end(), [](const std::pair<int32_t, double>& x, const std::pair<int32_t, double>& y) {
+            return x.first < y.first;
+        });
+        int64_t a = hp[(size_t)r], b = cp[(size_t)r];
+        for (const auto& cvp : tmp) {
+            if (cvp.first < kEvalHot) {
+                hc[(size_t)a] = (uint16_t)cvp.first;
+                hv[(size_t)a++] = cvp.second;
+            } else {
+                cc[(size_t)b] = cvp.first;
+                cv[(size_t)b++] = cvp.second;
+            }
+        }
+    }
+    ctx->hot_te = Csr{};
+    ctx->cold_te = Csr{};
+    ctx->hot_te.n = ctx->cold_te.n = n;
+    ctx->hot_te.nnz = nh;
+    ctx->cold_te.nnz = nc;
+    upload(ctx->hot_te.row_ptr, hp.data(), sizeof(int64_t) * (size_t)(n + 1), s);
+    upload_padded(ctx->hot_te.col16, hc.data(), sizeof(uint16_t) * (size_t)nh, s);
+    upload_padded(ctx->hot_te.val, hv.data(), sizeof(double) * (size_t)nh, s);
+    upload(ctx->cold_te.row_ptr, cp.data(), sizeof(int64_t) * (size_t)(n + 1), s);
+    upload_padded(ctx->cold_te.col, cc.data(), sizeof(int32_t) * (size_t)nc, s);
+    upload_col16(ctx->cold_te.col16, cc, nc, ctx->d, s);  // (synchronises: the host vectors may go)
+    upload_padded(ctx->cold_te.val, cv.data(), sizeof(double) * (size_t)nc, s);
+    int hcap = kEvalTile, ccap = kEvalTile;
+    eval_split_tiles(&hcap, &ccap);
+    ctx->n_hot_t_tiles = make_tiles(hp.data(), n, ctx->hot_t_tiles, s, hcap);  // (synchronises)
+    ctx->n_cold_t_tiles = make_tiles(cp.data(), n, ctx->cold_t_tiles, s, ccap);
+    ctx->row_base.alloc(sizeof(double) * (size_t)(ctx->tr.n + n));
+    ctx->te_split = ctx->n_hot_t_tiles > 0;
+}
+
 static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, const int64_t* part_ptr,
                            const int64_t* row_ptr, const int32_t* col, const double* val, const double* y,
                            int64_t n_rows, int32_t num_features, int32_t part_begin, int32_t num_parts_global) {
@@ -1133,6 +1201,7 @@ static void set_train_impl(cocoa_ctx* ctx, bool dense_in, int32_t num_parts, con
     // (eval_tile_entries), so keeping it could evaluate wrong columns or run
     // 4,096-entry tiles under the 2,048-entry kernel.  Call cocoa_set_test again.
     ctx->csc_ready = false;  // (the mb-SGD CSC copy is of the old rows)
+    ctx->te_split = false;
     if (ctx->has_test) {
         ctx->has_test = false;
         ctx->te_dense = false;
@@ -1309,6 +1378,7 @@ static void set_test_impl(cocoa_ctx* ctx, bool dense_in, const int64_t* row_ptr,
                           const double* val, const double* y, int64_t n_rows) {
     require(dense_in || col != nullptr, COCOA_E_ARG, "cocoa_set_test: null column array");
     ctx->eval_quiesce();  // a pending evaluation reads the test rows being replaced
+    ctx->te_split = false;
     require(ctx->d > 0, COCOA_E_STATE, "cocoa_set_test: call cocoa_set_train first");
     require(row_ptr && y && n_rows >= 0, COCOA_E_ARG, "cocoa_set_test: bad argument");
     if (!dense_in) check_csr(row_ptr, col, n_rows, ctx->d);
@@ -1328,6 +1398,7 @@ static void set_test_impl(cocoa_ctx* ctx, bool dense_in, const int64_t* row_ptr,
         for (int64_t q = 0; q < nnz; ++q) pcol[(size_t)q] = ctx->perm[(size_t)col[q]];  // device feature order
         upload_padded(ctx->te.col, pcol.data(), sizeof(int32_t) * (size_t)nnz, s);
         upload_col16(ctx->te.col16, pcol, nnz, ctx->d, s);
+        build_test_split(ctx, row_ptr, pcol, val, n_rows, s);
     }
     upload_padded(ctx->te.val, val, sizeof(double) * (size_t)nnz, s);
     upload(ctx->te.y, y, sizeof(double) * (size_t)n_rows, s);
@@ -2464,6 +2535,19 @@ static void eval_launch(cocoa_ctx* ctx, bool async = false, bool to_host = true)
         e.val = ctx->cold_tr.val.as<double>();
         e.tiles = ctx->cold_tiles.as<int64_t>();
         e.n_tiles = ctx->n_cold_tiles;
+        if (ctx->has_test && ctx->te_split) {  // the test rows' cold entries here, hot ones in the hot pass
+            e.t_row_ptr = ctx->cold_te.row_ptr.as<int64_t>();
+            e.t_col = ctx->cold_te.col.as<int32_t>();
+            e.t_col16 = ctx->cold_te.col16.p ? ctx->cold_te.col16.as<uint16_t>() : nullptr;
+            e.t_val = ctx->cold_te.val.as<double>();
+            e.t_tiles = ctx->cold_t_tiles.as<int64_t>();
+            e.n_t_tiles = ctx->n_cold_t_tiles;
+            e.th_row_ptr = ctx->hot_te.row_ptr.as<int64_t>();
+            e.th_col16 = ctx->hot_te.col16.as<uint16_t>();
+            e.th_val = ctx->hot_te.val.as<double>();
+            e.th_tiles = ctx->hot_t_tiles.as<int64_t>();
+            e.n_th_tiles = ctx->n_hot_t_tiles;
+        }
         if (ctx->n_warm_tiles > 0) {
             e.m_row_ptr = ctx->warm_tr.row_ptr.as<int64_t>();
             e.m_col16 = ctx->warm_tr.col16.as<uint16_t>();
@@ -3702,7 +3786,7 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   "\"lds_bytes\":%zu,\"stream_cap\":%d,\"any_dup\":%d,\"max_nl\":%d,"
                   "\"hot_nnz_frac_4096\":%.4f,\"dw_dbuf\":%d,\"solver\":\"%s\",\"dw_compact\":%d,\"max_u\":%lld,"
                   "\"sum_u\":%lld,\"fold\":\"%s\",\"xw_producer\":%d,\"side_cus_reserved\":%d,\"chain_hot\":%d,"
-                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld,\"mbsgd_pull\":%d,\"eval_split\":%d,\"eval_warm\":%d}",
+                  "\"dw_private\":%d,\"max_uh\":%lld,\"n_tail\":%lld,\"mbsgd_pull\":%d,\"eval_split\":%d,\"eval_warm\":%d,\"eval_test_split\":%d}",
                   ctx->use_gram ? ctx->gram_chunks : 0, ctx->gram_mirror && !ctx->device_shared() ? 1 : 0,
                   ctx->strict ? 1 : 0, ctx->method, ctx->K_loc, ctx->K_glob, ctx->d, ctx->vec_lds ? 1 : 0,
                   ctx->alpha_lds ? 1 : 0, ctx->lds_bytes, ctx->sa.stream_cap, ctx->any_dup ? 1 : 0, ctx->max_nl,
@@ -3712,7 +3796,8 @@ extern "C" int cocoa_plan_info(cocoa_ctx* ctx, char* buf, int len) {
                   !ctx->dw_compact ? "dense" : (ctx->n_fitems > 0 && ctx->dw_dbuf) ? "blocks" : "gather",
                   ctx->xw_prod ? 1 : 0, ctx->gstream ? ctx->side_res : 0, ctx->sa.hot, ctx->dw_priv ? 1 : 0,
                   (long long)ctx->max_uh, (long long)ctx->n_tail, ctx->mbsgd_pull ? 1 : 0,
-                  ctx->split_ready && !ctx->strict ? 1 : 0, ctx->split_ready && ctx->n_warm_tiles > 0 ? 1 : 0);
+                  ctx->split_ready && !ctx->strict ? 1 : 0, ctx->split_ready && ctx->n_warm_tiles > 0 ? 1 : 0,
+                  ctx->split_ready && ctx->has_test && ctx->te_split ? 1 : 0);
     require(wrote >= 0 && wrote < len, COCOA_E_ARG, "cocoa_plan_info: buffer too small");
     CAPI_END(ctx)
 }

@@ -319,6 +319,14 @@ struct EvalArgs {
     const double* m_val;
     const int64_t* m_tiles;
     int64_t n_m_tiles;
+    // the test rows split the same way (n_th_tiles > 0): their hot entries as a
+    // CSR of their own (th_*), summed by the hot pass into row_base[n + r]; the
+    // t_* arrays above then hold the test rows' cold entries
+    const int64_t* th_row_ptr;
+    const uint16_t* th_col16;
+    const double* th_val;
+    const int64_t* th_tiles;
+    int64_t n_th_tiles;
 };
 constexpr int kEvalHot = 4096;   // w columns in LDS in the split evaluation's hot pass
 constexpr int kEvalWarm = 65536; // columns of its warm pass (0.5 MB of w: L2-resident gathers)

@@ -316,10 +316,13 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
         const int64_t r0 = tl[tt], r1 = tl[tt + 1];
         const int64_t e0 = te[tt], e1 = te[tt + 1];
         const int64_t T = e1 - e0;
+        // the row's hot-pass dot: train rows at row_base[r], split test rows at [n + r]
+        const bool has_base = BASE && (!test || a.n_th_tiles > 0);
+        const double* rb = test ? a.row_base + a.n : a.row_base;
         if (T > TILE) {
             double acc = 0.0;
             for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += vl[q] * a.w[cl[q]];
-            const double dot = block_sum_n<BLOCK>(acc, red) + ((BASE && !test) ? a.row_base[r0] : 0.0);
+            const double dot = block_sum_n<BLOCK>(acc, red) + (has_base ? rb[r0] : 0.0);
             if (tid == 0) {
                 if (!test) {
                     hinge += jmax(1 - yy[r0] * dot, 0.0);
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             roff[i] = (uint16_t)(rp[r0 + i] - e0);
             if (i < nr) {
                 yl[i] = yy[r0 + i];
-                if (BASE && !test) bl[i] = a.row_base[r0 + i];
+                if (has_base) bl[i] = rb[r0 + i];
             }
         }
         const int64_t base = e0 & ~(int64_t)3;
@@ -373,8 +376,8 @@ __global__ __launch_bounds__(BLOCK) void eval_stream_kernel(EvalArgs a) {
             for (int q = b + sub; q < e; q += 16) acc += prod[q];
             double dot = row16_sum(acc);
             if (sub == 0) {
+                if (has_base) dot += bl[r];
                 if (!test) {
-                    if (BASE) dot += bl[r];
                     hinge += jmax(1 - yl[r] * dot, 0.0);
                     if (a.row_xw) a.row_xw[r0 + r] = dot;
                 } else {
@@ -622,26 +625,31 @@ __global__ __launch_bounds__(BLOCK) void eval_hot_kernel(EvalArgs a) {
     auto w_of = [&](int32_t c) -> double { return WARM ? wm[c] : whot[c]; };
     const int sub = tid & 15, grp = tid >> 4;
     const int64_t nt = WARM ? a.n_m_tiles : a.n_h_tiles;
-    const int64_t* tl = WARM ? a.m_tiles : a.h_tiles;
-    const int64_t* te = tl + nt + 1;
-    const int64_t* rp = WARM ? a.m_row_ptr : a.h_row_ptr;
-    const uint16_t* cl = WARM ? a.m_col16 : a.h_col16;
-    const double* vl = WARM ? a.m_val : a.h_val;
-    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
-        const int64_t r0 = tl[t], r1 = tl[t + 1];
-        const int64_t e0 = te[t], e1 = te[t + 1];
+    // (the hot pass also takes the split test rows' tiles, after the train ones)
+    const int64_t ntt = WARM ? 0 : a.n_th_tiles;
+    for (int64_t t = blockIdx.x; t < nt + ntt; t += gridDim.x) {
+        const bool test = t >= nt;
+        const int64_t tt = test ? t - nt : t;
+        const int64_t* tl = test ? a.th_tiles : WARM ? a.m_tiles : a.h_tiles;
+        const int64_t* te = tl + (test ? ntt : nt) + 1;
+        const int64_t* rp = test ? a.th_row_ptr : WARM ? a.m_row_ptr : a.h_row_ptr;
+        const uint16_t* cl = test ? a.th_col16 : WARM ? a.m_col16 : a.h_col16;
+        const double* vl = test ? a.th_val : WARM ? a.m_val : a.h_val;
+        double* rb = test ? a.row_base + a.n : a.row_base;
+        const int64_t r0 = tl[tt], r1 = tl[tt + 1];
+        const int64_t e0 = te[tt], e1 = te[tt + 1];
         const int64_t T = e1 - e0;
         if (T > TILE) {
             double acc = 0.0;
             for (int64_t q = e0 + tid; q < e1; q += BLOCK) acc += vl[q] * w_of(cl[q]);
             const double dot = block_sum_n<BLOCK>(acc, red);
-            if (tid == 0) a.row_base[r0] = WARM ? a.row_base[r0] + dot : dot;
+            if (tid == 0) rb[r0] = WARM ? rb[r0] + dot : dot;
             continue;
         }
         const int nr = (int)(r1 - r0);
         for (int i = tid; i <= nr; i += BLOCK) {
             roff[i] = (uint16_t)(rp[r0 + i] - e0);
-            if (WARM && i < nr) bl[i] = a.row_base[r0 + i];
+            if (WARM && i < nr) bl[i] = rb[r0 + i];
         }
         const int64_t base = e0 & ~(int64_t)3;
         const int sh = (int)(e0 - base);
@@ -674,7 +682,7 @@ __global__ __launch_bounds__(BLOCK) void eval_hot_kernel(EvalArgs a) {
             double acc = 0.0;
             for (int q = b + sub; q < e; q += 16) acc += prod[q];
             const double dot = row16_sum(acc);
-            if (sub == 0) a.row_base[r0 + r] = WARM ? bl[r] + dot : dot;
+            if (sub == 0) rb[r0 + r] = WARM ? bl[r] + dot : dot;
         }
         __syncthreads();
     }
@@ -717,10 +725,10 @@ static int resident_grid(F kernel, int threads, int want) {
 }
 
 // the split evaluation: hot pass, then the cold pass over a's (cold) train CSR
-// and the (unsplit) test rows
+// and the test rows (their cold entries when n_th_tiles > 0, else whole)
 static bool launch_eval_split(const EvalArgs& a, int blocks, hipStream_t s) {
     const bool c16 = a.col16 && (a.n_test == 0 || a.t_col16);
-    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_h_tiles, 256 * COCOA_HOT_WGS));
+    const int hb = (int)std::max<int64_t>(1, std::min<int64_t>(a.n_h_tiles + a.n_th_tiles, 256 * COCOA_HOT_WGS));
     eval_hot_kernel<COCOA_HOT_TILE, COCOA_HOT_BLOCK, kEvalHot><<<hb, COCOA_HOT_BLOCK, 0, s>>>(a);
     if (a.n_m_tiles > 0) {
         const int mb = resident_grid(eval_hot_kernel<COCOA_HOT_TILE, COCOA_HOT_BLOCK, kEvalHot, true>, COCOA_HOT_BLOCK,

@@ -31,14 +31,16 @@ def _state(tr, H, lam, rounds=3):
     return run
 
 
-def _eval(monkeypatch, tr, te, run, H, lam, split, warm=False):
+def _eval(monkeypatch, tr, te, run, H, lam, split, warm=False, test_split=True):
     monkeypatch.setenv("COCOA_EVAL_SPLIT", "1" if split else "0")
     monkeypatch.setenv("COCOA_EVAL_WARM", "1" if warm else "0")
     e = Engine(strict=False)
     e.set_train(tr)
     monkeypatch.delenv("COCOA_EVAL_SPLIT")
     monkeypatch.delenv("COCOA_EVAL_WARM")
+    monkeypatch.setenv("COCOA_EVAL_TEST_SPLIT", "1" if test_split else "0")
     e.set_test(te)
+    monkeypatch.delenv("COCOA_EVAL_TEST_SPLIT")
     e.init("cocoa+", tr.n, 0, H, lam)
     e.set_w(run.w())
     e.set_alpha(run.alpha())
@@ -80,6 +82,7 @@ def test_split_eval_matches_oracle_and_one_pass(data, monkeypatch):
     e1, ev1 = _eval(monkeypatch, tr, te, run, H, lam, True)
     e0, ev0 = _eval(monkeypatch, tr, te, run, H, lam, False)
     assert e1.plan()["eval_warm"] == 0
+    assert e1.plan()["eval_test_split"] == 1 and e0.plan()["eval_test_split"] == 0
     _check(ev1, rv, 1e-12)
     _check(ev0, rv, 1e-12)
     for k in ("primal", "dual", "gap"):
@@ -88,6 +91,49 @@ def test_split_eval_matches_oracle_and_one_pass(data, monkeypatch):
         e2, ev2 = _eval(monkeypatch, tr, te, run, H, lam, True, warm=True)
         assert e2.plan()["eval_warm"] == 1
         _check(ev2, rv, 1e-12)
+
+
+@pytest.mark.parametrize("data", ["c2", "long_test_row", "empty_test_rows"])
+def test_test_rows_split_matches_oracle_and_whole(data, monkeypatch):
+    """The test rows split like the train rows (EvalArgs::th_*, on by default;
+    COCOA_EVAL_TEST_SPLIT=0 keeps them whole in the cold pass): their hot
+    entries summed by the hot pass into row_base[n + r], the cold pass adding
+    them before the sign test.  Error counts exact against the oracle with the
+    split on and off: C2-shaped rows, a test row whose hot part alone passes a
+    tile (5,000 hot entries), and test rows with no entries or (mostly) cold ones."""
+    if data == "c2":
+        sh = configs.share("c2", n=60000, parts=16, n_test=5000)
+        tr, te = sh.train, sh.test
+        H, lam = sh.H, 1e-4
+    else:
+        tr = _dup_rows()
+        H, lam = 200, 2e-3
+        if data == "long_test_row":
+            te = tr.row_range(tr.n - 300, tr.n)
+        else:
+            base = tr.row_range(0, 400)
+            rp = base.row_ptr.copy()
+            keep = np.ones(len(base.col), bool)
+            for r in range(0, 400, 3):  # every third row empty; every third one cold-only
+                keep[rp[r]:rp[r + 1]] = False
+            dev_order = np.argsort(-np.bincount(tr.col, minlength=tr.num_features), kind="stable")
+            hot = np.zeros(tr.num_features, bool)
+            hot[dev_order[:4096]] = True
+            for r in range(1, 400, 3):
+                seg = slice(rp[r], rp[r + 1])
+                keep[seg] &= ~hot[base.col[seg]]
+            cnt = np.array([keep[rp[r]:rp[r + 1]].sum() for r in range(400)])
+            row_ptr = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+            te = LabeledData(row_ptr, base.col[keep], base.val[keep], base.y, np.array([0, 400], np.int64),
+                             tr.num_features)
+    run = _state(tr, H, lam)
+    rv = run.eval(odata(te))
+    e1, ev1 = _eval(monkeypatch, tr, te, run, H, lam, True)
+    e0, ev0 = _eval(monkeypatch, tr, te, run, H, lam, True, test_split=False)
+    assert e1.plan()["eval_test_split"] == 1 and e0.plan()["eval_test_split"] == 0
+    _check(ev1, rv, 1e-12)
+    _check(ev0, rv, 1e-12)
+    assert ev1["test_err_count"] == ev0["test_err_count"]
 
 
 def _warm_rows():
