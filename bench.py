@@ -288,6 +288,8 @@ def main():
                     help="bound on the CPU baseline's fresh run to the gap target")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gap", action="store_true")
+    ap.add_argument("--stats-kernels", default="solver,eval",
+                    help="kernels bracketed with HIP events in the timed region (A/B of the events' own cost)")
     ap.add_argument("--stats-all", action="store_true",
                     help="HIP events around every kernel in the timed region (default: the solver and the eval only)")
     ap.add_argument("--eval-sync", action="store_true",
@@ -428,7 +430,7 @@ def main():
     # events only around the two kernels the rooflines read: every bracketed
     # launch adds two event packets and ~5-10 us of launch latency
     if not args.stats_all and hasattr(cocoa_amd._capi.lib(), "cocoa_stats_kernels"):
-        eng.stats_kernels(["solver", "eval"])
+        eng.stats_kernels(args.stats_kernels.split(","))
     eng.stats_enable(True)
     barrier()
     tele_start = tele.snap()
@@ -442,6 +444,8 @@ def main():
     stats = eng.kernel_stats()
     # the eval pass alone (in the timed loop it overlaps the next round's solver)
     eng.stats_reset()
+    if not args.stats_all and hasattr(cocoa_amd._capi.lib(), "cocoa_stats_kernels"):
+        eng.stats_kernels(["eval"])
     eng.sync()
     for _ in range(5):
         runner.eval()
@@ -499,8 +503,9 @@ def main():
     # the eval's launch average over the timed region (HIP events on the
     # engine's stream); the 5 launches after it, with nothing beside them, are
     # reported as alone_ms
-    eval_ms = stats["eval"]["total_ms"] / max(stats["eval"]["launches"], 1)
     eval_alone_ms = (eval_alone.get("total_ms", 0.0) / max(eval_alone.get("launches", 0), 1)) if eval_alone else None
+    eval_in_line = stats.get("eval", {}).get("launches", 0) > 0  # (--stats-kernels without eval: alone only)
+    eval_ms = stats["eval"]["total_ms"] / stats["eval"]["launches"] if eval_in_line else eval_alone_ms
     b_eval = eval_bytes(tr, te, args.d, plan.get("solver") == "dense")
     ach_eval = b_eval / (eval_ms * 1e-3) / 1e9
 
@@ -603,9 +608,10 @@ def main():
                               "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": ach_eval / PEAK_HBM_GBS,
                               "traffic": traffic_eval, "bytes_per_launch": b_eval, "avg_launch_ms": eval_ms,
                               "alone_ms": eval_alone_ms,
-                              "note": "avg_launch_ms: HIP events over the timed rounds (" +
+                              "note": ("avg_launch_ms: alone_ms (no events on the evaluation in the timed region, "
+                                       "--stats-kernels)" if not eval_in_line else "avg_launch_ms: HIP events over the timed rounds (" +
                                       ("beside the next round's solver and Gram rows, --pipeline)" if pipe else
-                                       "in line on the engine's stream; the next Gram rows wait for the next plan)")
+                                       "in line on the engine's stream; the next Gram rows wait for the next plan)"))
                                       + "; alone_ms: 5 launches after the timed region with nothing beside them"},
             "kernel_ms": {k: (v["total_ms"] / v["launches"]) for k, v in stats.items() if v["launches"] > 0},
             "cpu_baseline": cpu,
