@@ -288,8 +288,10 @@ def main():
                     help="bound on the CPU baseline's fresh run to the gap target")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gap", action="store_true")
-    ap.add_argument("--stats-kernels", default="solver,eval",
-                    help="kernels bracketed with HIP events in the timed region (A/B of the events' own cost)")
+    ap.add_argument("--stats-kernels", default="solver",
+                    help="kernels bracketed with HIP events in the timed region (default: the dominant kernel "
+                         "the roofline reads; each bracketed launch adds two event packets to the step, "
+                         "solver,eval: 7.8 us more per C2 step, profiles/r06/ab_r10g_events.txt)")
     ap.add_argument("--stats-all", action="store_true",
                     help="HIP events around every kernel in the timed region (default: the solver and the eval only)")
     ap.add_argument("--eval-sync", action="store_true",
@@ -427,8 +429,9 @@ def main():
     t = 1
     _, _, t = steps(t, args.warmup)
     eng.stats_reset()
-    # events only around the two kernels the rooflines read: every bracketed
-    # launch adds two event packets and ~5-10 us of launch latency
+    # events only around the kernel the roofline reads (--stats-kernels): every
+    # bracketed launch adds two event packets and ~4-5 us of launch latency each;
+    # the evaluation's own roofline then reads the 5 launches after the timed region
     if not args.stats_all and hasattr(cocoa_amd._capi.lib(), "cocoa_stats_kernels"):
         eng.stats_kernels(args.stats_kernels.split(","))
     eng.stats_enable(True)

@@ -2027,7 +2027,6 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         // the Gram solver runs this round (local SGD's wrapped-counter rounds do not)
         const bool gram_round = c->use_gram && (c->method != COCOA_METHOD_LOCALSGD || lsgd_t0 >= 0);
         bool rows = false;  // x.w gathered from the last evaluation's row cache (the rest prefetched)
-        bool ew_done = false;  // e_w already recorded (COCOA_EW_EARLY)
         if (c->use_plan) {
             PlanArgs pa = plan_args(c, smp, b);
             // CoCoA's w moves inside the round: the chain solver forms x.w itself;
@@ -2042,14 +2041,6 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
             }
             // (the prefetched plan, formed beside the last solver, is exactly that)
             if (plan_ready && rows) {
-                // COCOA_EW_EARLY=1 (A/B): e_w marked before the gather, right behind
-                // the g_ready wait, instead of between the gather and the solver
-                static const bool ew_early = std::getenv("COCOA_EW_EARLY") && std::atoi(std::getenv("COCOA_EW_EARLY"));
-                if (ew_early && overlap && !produce && !(c->eval_pending && !c->eval_fired)) {
-                    if (!c->e_w) HIPCHK(hipEventCreateWithFlags(&c->e_w, hipEventDisableTiming));
-                    HIPCHK(hipEventRecord(c->e_w, s));
-                    ew_done = true;
-                }
                 c->timed(COCOA_K_PLAN, [&] {
                     launch_xw_gather(pa.part_ptr, smp, H, pa.steps, c->row_xw.as<double>(), c->plan_xw.as<double>(), s);
                 });
@@ -2069,8 +2060,8 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         // the side work of this round (x.w producer, a pipelined evaluation)
         // starts once the plan is done: begun earlier, it slowed the plan (on the
         // critical path) 0.04 -> 0.2 ms
-        c->e_w_rec = ew_done;
-        if (!ew_done && (produce || (c->eval_pending && !c->eval_fired) || overlap)) {
+        c->e_w_rec = false;
+        if (produce || (c->eval_pending && !c->eval_fired) || overlap) {
             if (!c->e_w) HIPCHK(hipEventCreateWithFlags(&c->e_w, hipEventDisableTiming));
             HIPCHK(hipEventRecord(c->e_w, s));
             c->e_w_rec = true;

@@ -23,6 +23,7 @@ def main():
         tel = d.get("gpu_telemetry") or {}
         runs.append({"variant": labels[i - 1] if i <= len(labels) else str(i), "rep": rep,
                      "ms_per_step": d["ms_per_step"], "kernel_ms": d.get("kernel_ms"),
+                     "eval_ms": (d.get("roofline_eval") or {}).get("avg_launch_ms"),
                      "value": d["value"], "steps": d["steps"], "warmup": d["warmup"],
                      "gpu_telemetry": {"bdf": tel.get("bdf"), "timed_start": tel.get("timed_start"),
                                        "timed_end": tel.get("timed_end"), "timed_samples": tel.get("timed_samples")}})
@@ -31,14 +32,16 @@ def main():
         s = summary.setdefault(r["variant"], {"ms_per_step": [], "solver_ms": [], "eval_ms": []})
         s["ms_per_step"].append(r["ms_per_step"])
         s["solver_ms"].append((r["kernel_ms"] or {}).get("solver"))
-        s["eval_ms"].append((r["kernel_ms"] or {}).get("eval"))
+        s["eval_ms"].append((r["kernel_ms"] or {}).get("eval", r.get("eval_ms")))
     for s in summary.values():
         for k in list(s):
             v = [x for x in s[k] if x is not None]
             s[k + "_mean"] = sum(v) / len(v) if v else None
     json.dump({"tag": tag, "runs": runs, "summary": summary}, open(out, "w"), indent=1)
     for k, s in summary.items():
-        print(f"{k:40s} ms/step {s['ms_per_step_mean']:.4f}  solver {s['solver_ms_mean']:.4f}  eval {s['eval_ms_mean']:.4f}")
+        ev = s["eval_ms_mean"]
+        print(f"{k:40s} ms/step {s['ms_per_step_mean']:.4f}  solver {s['solver_ms_mean']:.4f}  eval "
+              + (f"{ev:.4f}" if ev is not None else "-"))
 
 
 if __name__ == "__main__":

@@ -84,7 +84,7 @@ for step in "$@"; do
       for v in ${EVAL_VARIANTS:-0 1 2}; do
         COCOA_EVAL_VARIANT=$v timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-gap ${BENCH_ARGS} \
           > $O/evalab_${v}_$TAG.json 2> $O/evalab_${v}_$TAG.err || exit $?
-        python3 -c "import json;d=json.loads(open('$O/evalab_${v}_$TAG.json').readlines()[-1]);print('eval variant $v', round(d['kernel_ms']['eval'],4), 'ms', round(d['roofline_eval']['frac'],3), 'step', round(d['ms_per_step'],3), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
+        python3 -c "import json;d=json.loads(open('$O/evalab_${v}_$TAG.json').readlines()[-1]);print('eval variant $v', round(d['roofline_eval']['avg_launch_ms'],4), 'ms', round(d['roofline_eval']['frac'],3), 'step', round(d['ms_per_step'],3), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
       done ;;
     evalpmc)  # PMC counters of the eval kernel (one pass per counter group)
       for grp in "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "TCC_HIT_sum TCC_MISS_sum" "TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU"; do
@@ -111,7 +111,7 @@ for step in "$@"; do
         v=${v//=/_}
         env $envset COCOA_LIB=$lib timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-gap ${BENCH_ARGS} \
           > $O/ab_${v}_$TAG.json 2> $O/ab_${v}_$TAG.err || exit $?
-        python3 -c "import json;d=json.loads(open('$O/ab_${v}_$TAG.json').readlines()[-1]);k=d['kernel_ms'];print('$v', 'step', round(d['ms_per_step'],4), 'solver', round(k['solver'],4), 'gram', round(k.get('gram',0),4), 'eval', round(k['eval'],4), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
+        python3 -c "import json;d=json.loads(open('$O/ab_${v}_$TAG.json').readlines()[-1]);k=d['kernel_ms'];print('$v', 'step', round(d['ms_per_step'],4), 'solver', round(k['solver'],4), 'gram', round(k.get('gram',0),4), 'eval', round(d['roofline_eval']['avg_launch_ms'],4), 'gap[-1]', repr(d['gap_trajectory_timed'][-1]))"
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
