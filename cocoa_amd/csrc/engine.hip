@@ -315,6 +315,11 @@ struct cocoa_ctx {
     // cocoa_eval_end (single rank, one device); other contexts hold the finished
     // result in eval_held
     bool inl_pending = false;
+    // an in-line evaluation was enqueued since the last round (cocoa_eval_begin, one
+    // rank): its e_inl, recorded behind it, gates the next Gram rows on the side
+    // stream in place of an e_w record behind the x.w gather (one marker packet
+    // fewer on the main stream; COCOA_GATE_INL=0 restores the e_w record)
+    bool inl_since_round = false;
     bool inl_ranks = false;       //   its sums all-reduced across ranks on the device (fast multi-rank)
     int64_t n_test_glob = -1;     // test rows over all ranks (-1: not yet exchanged for this test set)
     hipEvent_t e_inl = nullptr;
@@ -2061,7 +2066,13 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
         // starts once the plan is done: begun earlier, it slowed the plan (on the
         // critical path) 0.04 -> 0.2 ms
         c->e_w_rec = false;
-        if (produce || (c->eval_pending && !c->eval_fired) || overlap) {
+        // (COCOA_GATE_INL=0: the e_w record instead; 1.9632 -> 1.9584 ms per C2 step with the
+        // e_inl gate, profiles/r06/ab_r10j_gate_inl.txt)
+        static const bool gate_inl_env = !std::getenv("COCOA_GATE_INL") || std::atoi(std::getenv("COCOA_GATE_INL"));
+        const bool gate_inl = gate_inl_env && c->inl_since_round && c->e_inl && overlap && !produce &&
+                              !(c->eval_pending && !c->eval_fired);
+        c->inl_since_round = false;
+        if (!gate_inl && (produce || (c->eval_pending && !c->eval_fired) || overlap)) {
             if (!c->e_w) HIPCHK(hipEventCreateWithFlags(&c->e_w, hipEventDisableTiming));
             HIPCHK(hipEventRecord(c->e_w, s));
             c->e_w_rec = true;
@@ -2173,6 +2184,7 @@ static void run_local(cocoa_ctx* c, int32_t t, bool fuse_apply, const double* ch
                     // _end), the Gram rows would otherwise start during that
                     // evaluation and hold CUs the next solver's workgroups need whole
                     if (c->e_w_rec) HIPCHK(hipStreamWaitEvent(c->gstream, c->e_w, 0));
+                    if (gate_inl) HIPCHK(hipStreamWaitEvent(c->gstream, c->e_inl, 0));  // (the last evaluation: done)
                     int32_t* nsmp = nb ? c->samples2.as<int32_t>() : c->samples.as<int32_t>();
                     double* ngt = nb ? c->gt2.as<double>() : c->gt.as<double>();
                     const int32_t nseed = wrap32((int64_t)c->D.seed + t + 1);
@@ -2799,6 +2811,7 @@ extern "C" int cocoa_eval_begin(cocoa_ctx* ctx) {
         if (!ctx->e_inl) HIPCHK(hipEventCreateWithFlags(&ctx->e_inl, hipEventDisableTiming));
         eval_launch(ctx);
         HIPCHK(hipEventRecord(ctx->e_inl, ctx->stream));
+        ctx->inl_since_round = true;
     }
     ctx->inl_pending = true;
     CAPI_END(ctx)
